@@ -1,0 +1,169 @@
+/*
+ * moeva_mi355x.h -- C ABI of the MI355X-native MoEvA2 engine (libmoeva_mi355x.so).
+ *
+ * The reference is pure Python: its hot path is reached through
+ *   Moeva2.generate(x, minimize_class)             src/attacks/moeva2/moeva2.py:174-207
+ *   DefaultProblem._evaluate(x, out)               src/attacks/moeva2/default_problem.py:99-140
+ * and, inside pymoo 0.4.2.2 (not vendored), R-NSGA-III survival + mating.  Each entry
+ * point below replaces one of those surfaces; the Python host package
+ * (moeva2_amd.attacks.moeva2.*) binds them with ctypes exactly as a maintainer would add
+ * to the reference.
+ *
+ * Conventions
+ *  - status codes (MV_OK == 0); mv_last_error() returns a thread-local message;
+ *  - no exceptions cross the ABI; no torch types; plain pointers and sizes;
+ *  - pointers documented "dev" are device (HBM) pointers owned by the caller
+ *    (e.g. torch tensors' data_ptr()); "host" pointers are read synchronously;
+ *  - every launch is ordered on the caller's hipStream_t (passed as void*; NULL = default
+ *    stream) and is asynchronous unless stated;
+ *  - one mv_engine per (device, problem); an engine is thread-compatible, not thread-safe.
+ */
+#ifndef MOEVA_MI355X_H
+#define MOEVA_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MV_OK = 0,
+  MV_ERR_ARG = 1,   /* invalid argument / shape */
+  MV_ERR_HIP = 2,   /* HIP runtime error */
+  MV_ERR_STATE = 3, /* call out of order (e.g. no states bound) */
+};
+
+/* gene kinds (feature_encoder.py:169-181 get_type_mask_genetic) */
+enum { MV_GENE_REAL = 0, MV_GENE_INT = 1, MV_GENE_OHE = 2 };
+
+/* constraint op codes: one op == one constraint column, evaluated on the ML-space row
+ * x_f (default_problem.py:93-97 then constraints.evaluate numpy path). */
+enum {
+  MV_OP_DIFF = 1,          /* x[a0] - x[a1]                        botnet_constraints.py:283-285 */
+  MV_OP_RATIO_SAFE = 2,    /* (x[a1]!=0 ? x[a0]/x[a1] : 0) - k0     botnet_constraints.py:304-306 */
+  MV_OP_ABS_SUMDIFF = 3,   /* |sum(pool[a0:a1]) - sum(pool[a1:a2])| botnet_constraints.py:127-148 */
+  MV_OP_LCLD_INSTALL = 4,  /* |x3 - x0 r (1+r)^x1/((1+r)^x1-1)| - k0, r=x2/1200  lcld:174-177 */
+  MV_OP_LCLD_TERM = 5,     /* |(36-x[a0])(60-x[a0])|               lcld_constraints.py:186 */
+  MV_OP_ABS_RATIO = 6,     /* |x[a0] - x[a1]/x[a2]|                lcld_constraints.py:189-207 */
+  MV_OP_MONTHDIFF = 7,     /* |x[a0] - (month(x[a1]) - month(x[a2]))| lcld_constraints.py:195-201 */
+  MV_OP_RATIO_MASKED = 8,  /* |x[a0] - (x[a2]==0|inf|nan ? -1 : x[a1]/x[a2])| lcld:210-216 */
+  MV_OP_XOR_AUG = 9,       /* |x[a0] - xor(x[a1]>=k0, x[a2]>=k1)|  examples/utils.py:7-29 */
+};
+
+typedef struct mv_problem_desc {
+  int32_t D;                  /* ML feature count */
+  int32_t V;                  /* genetic length (n_var) */
+  int32_t Dm;                 /* mutable feature count (mutable_mask.sum()) */
+  int32_t C;                  /* constraint count */
+  int32_t n_ohe;              /* mutable one-hot groups */
+  const int32_t* gene_kind;   /* host [V] MV_GENE_* */
+  const int32_t* gene_feat;   /* host [V] feature (REAL/INT) or group index (OHE) */
+  const int32_t* ohe_offsets; /* host [n_ohe+1] CSR offsets into ohe_feats */
+  const int32_t* ohe_feats;   /* host [..] features of each group, category order */
+  const int32_t* mut_feats;   /* host [Dm] mutable features, ascending */
+  const double* ml_scale;     /* host [D] ML MinMaxScaler scale_ (NULL: identity) */
+  const double* ml_min;       /* host [D] ML MinMaxScaler min_   (NULL: identity) */
+  const int32_t* op_code;     /* host [C] MV_OP_* */
+  const int32_t* op_arg;      /* host [C*4] integer operands */
+  const double* op_karg;      /* host [C*2] real operands */
+  int32_t n_pool;             /* index pool size for MV_OP_ABS_SUMDIFF */
+  const int32_t* idx_pool;    /* host [n_pool] */
+  double tol;                 /* constraints <= tol -> 0  (1e-3 in every reference class) */
+  int32_t norm;               /* 2 = L2, 0 = Linf  (default_problem.py:80-91) */
+  int32_t scale_objectives;   /* f2 MinMax scaling (utils.py:11-22) */
+} mv_problem_desc;
+
+typedef struct mv_model_desc {
+  int32_t n_layers;           /* Dense layers; hidden relu, last softmax */
+  const int32_t* dims;        /* host [n_layers+1], dims[0] == D */
+  const float* const* W;      /* host per layer [dims[l] x dims[l+1]] row-major (Keras kernel) */
+  const float* const* b;      /* host per layer [dims[l+1]] */
+} mv_model_desc;
+
+typedef struct mv_engine mv_engine;
+
+const char* mv_last_error(void);
+int mv_device_count(int32_t* n);
+
+/* Upload problem constants + classifier weights to `device` (model may be NULL for a
+ * constraints-only engine). */
+int mv_engine_create(int32_t device, const mv_problem_desc* problem, const mv_model_desc* model,
+                     mv_engine** out);
+void mv_engine_destroy(mv_engine* e);
+
+/* Bind B initial states (host arrays, copied).  xl/xu are the per-state feature bounds
+ * Constraints.get_feature_min_max(dynamic_input=x) (moeva2.py:141-142).  Derives on device:
+ * encoder MinMax (feature_encoder.py:39-40), genetic bounds (:145-163), the initial
+ * genetic vector (sampling.py:64-78) and the immutable-feature fold of the first layer. */
+int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* xl,
+                  const double* xu, const int32_t* minimize_class, void* stream);
+
+/* DefaultProblem._evaluate for n rows per bound state.
+ * genes dev [B][n][V] -> F dev [B][n][3] (f1 misclassification, f2 distance, f3 constraint sum);
+ * G dev [B][n][C] (constraint values after the tol clamp and G*(G>0)) or NULL. */
+int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double* G, void* stream);
+
+/* Constraints.evaluate (numpy path: values <= tol set to 0) on ML-space rows:
+ * x dev [n][D] -> G dev [n][C].  Works on an engine created without a model. */
+int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream);
+
+/* R-NSGA-III AspirationPointSurvival._do + NonDominatedSorting + niching, batched over B
+ * independent populations of N merged individuals (pymoo 0.4.2.2 rnsga3.py/nsga3.py).
+ * F dev [B][N][3]; ref_points dev [R][3]; state in/out dev: ideal [B][3], worst [B][3],
+ * extreme [B][3][3], has_extreme [B] (0 before the first call).
+ * Outputs dev: survivors [B][n_survive] (merged indices, new population order),
+ * rank [B][N] (front index, -1 = unranked) and, for the fronts-ordered individuals
+ * (order [B][N], count n_ranked [B]): niche [B][N], dist [B][N].  Any output may be NULL
+ * except survivors.  Requires N <= 512, R <= 640. */
+int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t R,
+               const double* ref_points, double mu, uint64_t seed, int32_t gen,
+               double* ideal, double* worst, double* extreme, int32_t* has_extreme,
+               int32_t* survivors, int32_t* rank, int32_t* order, int32_t* n_ranked,
+               int32_t* niche, double* dist, double* nadir, void* stream);
+
+/* TournamentSelection(comp_by_cv_then_random) for B populations of P: parents dev
+ * [B][ceil(O/2)][2] (population positions). */
+int mv_select_parents(int32_t B, int32_t P, int32_t O, uint64_t seed, int32_t gen,
+                      int32_t* parents, void* stream);
+
+/* MixedVariableCrossover(two-point) + MixedVariableMutation(PM, eta 20), no evaluation:
+ * pop dev [B][P][V], parents dev [B][O/2][2] -> off dev [B][O][V]. */
+int mv_variation(mv_engine* e, int32_t P, int32_t O, uint64_t seed, int32_t gen,
+                 const double* pop, const int32_t* parents, double* off, void* stream);
+
+/* Classifier.predict_proba (classifier.py:23-29) for a Dense(relu)...Dense(softmax)
+ * model: x dev [n][dims[0]] (ML-scaled, fp64, cast to fp32 like Keras) -> proba dev
+ * [n][n_out] fp64. */
+typedef struct mv_mlp mv_mlp;
+int mv_mlp_create(int32_t device, const mv_model_desc* model, mv_mlp** out);
+void mv_mlp_destroy(mv_mlp* m);
+int mv_mlp_predict(mv_mlp* m, int32_t n, const double* x, double* proba, void* stream);
+
+typedef struct mv_attack_params {
+  int32_t n_gen;          /* Moeva2 n_gen (termination "n_gen") */
+  int32_t pop_size;       /* P = n_ref_points + n_obj (203 for n_pop 200) */
+  int32_t n_offsprings;   /* O (even) */
+  uint64_t seed;          /* Moeva2 seed */
+  int32_t n_ref;          /* R reference points */
+  const double* ref_points; /* host [R][3] */
+  double mu;              /* RNSGA3 mu (0.05) */
+  int32_t history;        /* 0 none, 1 "reduced" (F), 2 "full" (F|G) */
+} mv_attack_params;
+
+/* Whole attack on device: init population + evaluate + (n_gen-1) x {select, vary+evaluate,
+ * survive}, no host round trip.  Asynchronous on `stream`. */
+int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
+/* Final population: genes dev [B][P][V], F dev [B][P][3] (either may be NULL). */
+int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
+/* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
+int mv_attack_history(mv_engine* e, double* hist, void* stream);
+/* Per-kernel timing of the last mv_attack_run when enabled (HIP events on `stream`). */
+int mv_set_profiling(mv_engine* e, int32_t enabled);
+int mv_get_kernel_times(mv_engine* e, double* vareval_ms, double* survive_ms,
+                        int32_t* n_vareval, int32_t* n_survive);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOEVA_MI355X_H */

@@ -1,0 +1,626 @@
+// C ABI of the MoEvA2 engine (see include/moeva_mi355x.h for the contract and the
+// reference surfaces each entry point replaces).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/moeva_mi355x.h"
+#include "engine.h"
+#include "kernels.h"
+
+using namespace mv;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return fail(MV_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc((void**)p, n * sizeof(T));
+}
+
+template <class T>
+hipError_t upload(T** p, const T* host, size_t n) {
+  hipError_t e = dalloc(p, n);
+  if (e != hipSuccess) return e;
+  if (n && host) return hipMemcpy(*p, host, n * sizeof(T), hipMemcpyHostToDevice);
+  return hipSuccess;
+}
+
+__global__ void k_fill_d(double* p, size_t n, double v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ void k_fill_i(int* p, size_t n, int v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+}  // namespace
+
+struct mv_engine {
+  int device = 0;
+  DProblem p{};
+  std::vector<void*> prob_allocs;
+  float* W1full = nullptr;
+  float* b1 = nullptr;
+  int H1 = 0;
+  // states
+  int B = 0;
+  std::vector<void*> state_allocs;
+  DStates s{};
+  double* genes0 = nullptr;
+  // attack
+  std::vector<void*> attack_allocs;
+  int P = 0, O = 0, S = 0, n_gen = 0, R = 0, hist_mode = 0, hist_w = 0, hist_rows = 0;
+  double* pool = nullptr;
+  double* poolF = nullptr;
+  int* pop_slot = nullptr;
+  int* free_slot = nullptr;
+  int* parents = nullptr;
+  double *ideal = nullptr, *worst = nullptr, *extreme = nullptr;
+  int* has_ext = nullptr;
+  double* ref = nullptr;
+  double* hist = nullptr;
+  bool attack_ready = false;
+  bool has_model = false;
+  // profiling
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_var, ev_surv;
+  int n_var_rec = 0, n_surv_rec = 0;
+
+  void free_list(std::vector<void*>& v) {
+    for (void* x : v) (void)hipFree(x);
+    v.clear();
+  }
+  template <class T>
+  hipError_t keep(std::vector<void*>& list, T** p, const T* host, size_t n) {
+    hipError_t e = upload(p, host, n);
+    if (e == hipSuccess) list.push_back((void*)*p);
+    return e;
+  }
+  ~mv_engine() {
+    (void)hipSetDevice(device);
+    free_list(attack_allocs);
+    free_list(state_allocs);
+    free_list(prob_allocs);
+    for (auto e : ev_var) (void)hipEventDestroy(e);
+    for (auto e : ev_surv) (void)hipEventDestroy(e);
+  }
+};
+
+extern "C" {
+
+const char* mv_last_error(void) { return g_err.c_str(); }
+
+int mv_device_count(int32_t* n) {
+  int c = 0;
+  HIPCHK(hipGetDeviceCount(&c));
+  *n = c;
+  return MV_OK;
+}
+
+int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_desc* md,
+                     mv_engine** out) {
+  if (!pd || !out) return fail(MV_ERR_ARG, "null argument");
+  *out = nullptr;
+  const int D = pd->D, V = pd->V, Dm = pd->Dm, C = pd->C;
+  if (D <= 0 || V <= 0 || Dm <= 0 || C < 0) return fail(MV_ERR_ARG, "bad problem sizes");
+  if (pd->D * 4 * 8 > 160 * 1024) return fail(MV_ERR_ARG, "D too large");
+  if (md && (md->n_layers < 2 || md->n_layers > MAX_LAYERS))
+    return fail(MV_ERR_ARG, "classifier must have 2..6 Dense layers");
+  if (md) {
+    if (md->dims[0] != D) return fail(MV_ERR_ARG, "model input width != D");
+    for (int l = 1; l < md->n_layers; ++l)
+      if (md->dims[l] % 16 != 0 || md->dims[l] > 512 || md->dims[l] <= 0)
+        return fail(MV_ERR_ARG, "hidden widths must be multiples of 16 and <= 512");
+    if (md->dims[md->n_layers] < 2 || md->dims[md->n_layers] > 8)
+      return fail(MV_ERR_ARG, "softmax output width must be 2..8");
+  }
+  for (int j = 1; j < Dm; ++j)
+    if (pd->mut_feats[j] <= pd->mut_feats[j - 1]) return fail(MV_ERR_ARG, "mut_feats not ascending");
+  HIPCHK(hipSetDevice(device));
+  mv_engine* e = new mv_engine();
+  e->device = device;
+  DProblem& p = e->p;
+  p.D = D;
+  p.V = V;
+  p.Dm = Dm;
+  p.Dm4 = (Dm + 3) & ~3;
+  p.C = C;
+  p.n_ohe = pd->n_ohe;
+  std::vector<int> sub(V);
+  int ns[2] = {0, 0};
+  for (int g = 0; g < V; ++g) {
+    const int k = pd->gene_kind[g];
+    if (k < 0 || k > 2) {
+      delete e;
+      return fail(MV_ERR_ARG, "bad gene kind");
+    }
+    const int ss = k == MV_GENE_REAL ? 0 : 1;
+    sub[g] = ns[ss]++;
+  }
+  p.n_sub[0] = ns[0];
+  p.n_sub[1] = ns[1];
+  std::vector<double> mls(D, 1.0), mlm(D, 0.0);
+  if (pd->ml_scale) std::memcpy(mls.data(), pd->ml_scale, D * sizeof(double));
+  if (pd->ml_min) std::memcpy(mlm.data(), pd->ml_min, D * sizeof(double));
+  const int n_ohe_feats = pd->n_ohe > 0 ? pd->ohe_offsets[pd->n_ohe] : 0;
+  std::vector<int> ohe_off(pd->n_ohe + 1, 0);
+  if (pd->n_ohe > 0) std::memcpy(ohe_off.data(), pd->ohe_offsets, (pd->n_ohe + 1) * sizeof(int));
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err == hipSuccess) err = e->keep(e->prob_allocs, dst, host, n);
+  };
+  K((int**)&p.gene_kind, pd->gene_kind, V);
+  K((int**)&p.gene_feat, pd->gene_feat, V);
+  K((int**)&p.gene_sub, sub.data(), V);
+  K((int**)&p.ohe_off, ohe_off.data(), ohe_off.size());
+  K((int**)&p.ohe_feat, pd->ohe_feats, n_ohe_feats);
+  K((int**)&p.mut_feat, pd->mut_feats, Dm);
+  K((double**)&p.ml_scale, mls.data(), D);
+  K((double**)&p.ml_min, mlm.data(), D);
+  K((int**)&p.op_code, pd->op_code, C);
+  K((int**)&p.op_arg, pd->op_arg, (size_t)C * 4);
+  K((double**)&p.op_k, pd->op_karg, (size_t)C * 2);
+  K((int**)&p.idx_pool, pd->idx_pool, pd->n_pool);
+  p.tol = pd->tol;
+  p.norm = pd->norm;
+  p.scale_obj = pd->scale_objectives;
+  p.f2_scale = pd->norm == 2 ? 1.0 / (std::sqrt((double)D) - 0.0) : 1.0;
+  if (md) {
+    e->has_model = true;
+    p.n_layers = md->n_layers;
+    for (int l = 0; l <= md->n_layers; ++l) p.dims[l] = md->dims[l];
+    e->H1 = md->dims[1];
+    // layer 0: mutable rows, zero padded to Dm4
+    std::vector<float> w1m((size_t)p.Dm4 * e->H1, 0.f);
+    for (int j = 0; j < Dm; ++j)
+      std::memcpy(&w1m[(size_t)j * e->H1], md->W[0] + (size_t)pd->mut_feats[j] * e->H1,
+                  e->H1 * sizeof(float));
+    K((float**)&p.W[0], w1m.data(), w1m.size());
+    K(&e->W1full, md->W[0], (size_t)D * e->H1);
+    K(&e->b1, md->b[0], e->H1);
+    p.bias[0] = e->b1;
+    for (int l = 1; l < md->n_layers; ++l) {
+      K((float**)&p.W[l], md->W[l], (size_t)md->dims[l] * md->dims[l + 1]);
+      K((float**)&p.bias[l], md->b[l], md->dims[l + 1]);
+    }
+  } else {
+    p.n_layers = 0;
+    e->H1 = 16;
+    std::vector<float> zero(16, 0.f);
+    K(&e->W1full, zero.data(), 16);
+    K(&e->b1, zero.data(), 16);
+  }
+  if (err != hipSuccess) {
+    delete e;
+    return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
+  }
+  int hmax = 16;
+  for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
+  const size_t lds = eval_lds_bytes(D, p.Dm4, hmax);
+  if (md && lds > 160 * 1024) {
+    delete e;
+    return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
+  }
+  *out = e;
+  return MV_OK;
+}
+
+void mv_engine_destroy(mv_engine* e) { delete e; }
+
+int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* xl,
+                  const double* xu, const int32_t* minimize_class, void* stream) {
+  if (!e || B <= 0 || !x_init || !xl || !xu || !minimize_class)
+    return fail(MV_ERR_ARG, "bad mv_set_states arguments");
+  if (!e->has_model) return fail(MV_ERR_STATE, "engine has no classifier");
+  HIPCHK(hipSetDevice(e->device));
+  const int nout = e->p.dims[e->p.n_layers];
+  for (int b = 0; b < B; ++b)
+    if (minimize_class[b] < 0 || minimize_class[b] >= nout)
+      return fail(MV_ERR_ARG, "minimize_class out of range");
+  HIPCHK(hipDeviceSynchronize());
+  e->free_list(e->state_allocs);
+  e->free_list(e->attack_allocs);
+  e->attack_ready = false;
+  const DProblem& p = e->p;
+  DStates& s = e->s;
+  s.B = B;
+  double *dxl = nullptr, *dxu = nullptr;
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err == hipSuccess) err = e->keep(e->state_allocs, dst, host, n);
+  };
+  K((double**)&s.x_init, x_init, (size_t)B * p.D);
+  K(&dxl, xl, (size_t)B * p.D);
+  K(&dxu, xu, (size_t)B * p.D);
+  K((int**)&s.min_class, minimize_class, B);
+  K((double**)&s.gl, (const double*)nullptr, (size_t)B * p.V);
+  K((double**)&s.gu, (const double*)nullptr, (size_t)B * p.V);
+  K((double**)&s.enc_scale, (const double*)nullptr, (size_t)B * p.Dm);
+  K((double**)&s.enc_min, (const double*)nullptr, (size_t)B * p.Dm);
+  K((double**)&s.x0_mm, (const double*)nullptr, (size_t)B * p.Dm);
+  K((float**)&s.bias1, (const float*)nullptr, (size_t)B * e->H1);
+  K(&e->genes0, (const double*)nullptr, (size_t)B * p.V);
+  if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
+  HIPCHK(launch_setup_states(p, B, s.x_init, dxl, dxu, e->W1full, e->b1, (double*)s.gl,
+                             (double*)s.gu, (double*)s.enc_scale, (double*)s.enc_min,
+                             (double*)s.x0_mm, (float*)s.bias1, e->genes0, (hipStream_t)stream));
+  e->B = B;
+  return MV_OK;
+}
+
+static RowsArgs base_rows(const mv_engine* e) {
+  RowsArgs a{};
+  a.p = e->p;
+  a.s = e->s;
+  a.eta = 20.0;
+  a.cx_prob = 0.9;
+  a.mut_thr = (uint32_t)(4294967296.0 / (double)e->p.V);
+  a.do_eval = 1;
+  return a;
+}
+
+int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double* G, void* stream) {
+  if (!e || n <= 0 || !genes || !F) return fail(MV_ERR_ARG, "bad mv_evaluate arguments");
+  if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  HIPCHK(hipSetDevice(e->device));
+  RowsArgs a = base_rows(e);
+  a.n = n;
+  a.total = e->B * n;
+  a.mode = 0;
+  a.genes_in = genes;
+  a.in_rows = n;
+  a.out_rows = n;
+  a.F = F;
+  a.G = G;
+  HIPCHK(launch_rows(a, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream) {
+  if (!e || n < 0 || (n > 0 && (!x || !G))) return fail(MV_ERR_ARG, "bad mv_constraints arguments");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(launch_constraints(e->p, n, x, G, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_variation(mv_engine* e, int32_t P, int32_t O, uint64_t seed, int32_t gen, const double* pop,
+                 const int32_t* parents, double* off, void* stream) {
+  if (!e || P <= 1 || O <= 0 || (O & 1) || !pop || !parents || !off)
+    return fail(MV_ERR_ARG, "bad mv_variation arguments (O must be even)");
+  if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  HIPCHK(hipSetDevice(e->device));
+  RowsArgs a = base_rows(e);
+  a.n = O;
+  a.total = e->B * O;
+  a.mode = 1;
+  a.genes_in = pop;
+  a.in_rows = P;
+  a.parents = parents;
+  a.genes_out = off;
+  a.out_rows = O;
+  a.seed = seed;
+  a.gen = gen;
+  a.do_eval = 0;
+  HIPCHK(launch_variation(a, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t R,
+               const double* ref_points, double mu, uint64_t seed, int32_t gen, double* ideal,
+               double* worst, double* extreme, int32_t* has_extreme, int32_t* survivors,
+               int32_t* rank, int32_t* order, int32_t* n_ranked, int32_t* niche, double* dist,
+               double* nadir, void* stream) {
+  if (B <= 0 || N <= 0 || N > SURV_NMAX || R <= 0 || R > SURV_RMAX || n_survive <= 0 ||
+      n_survive > N || !F || !ref_points || !ideal || !worst || !extreme || !has_extreme ||
+      !survivors)
+    return fail(MV_ERR_ARG, "bad mv_survive arguments (N <= 512, R <= 640, n_survive <= N)");
+  SurvArgs a{};
+  a.N = N;
+  a.n_survive = n_survive;
+  a.F = F;
+  a.ref = ref_points;
+  a.R = R;
+  a.mu = mu;
+  a.seed = seed;
+  a.gen = gen;
+  a.ideal = ideal;
+  a.worst = worst;
+  a.extreme = extreme;
+  a.has_extreme = has_extreme;
+  a.survivors = survivors;
+  a.rank = rank;
+  a.order = order;
+  a.n_ranked = n_ranked;
+  a.niche = niche;
+  a.dist = dist;
+  a.nadir = nadir;
+  HIPCHK(launch_survive(a, B, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_select_parents(int32_t B, int32_t P, int32_t O, uint64_t seed, int32_t gen,
+                      int32_t* parents, void* stream) {
+  if (B <= 0 || P <= 1 || O <= 0 || !parents) return fail(MV_ERR_ARG, "bad mv_select_parents");
+  HIPCHK(launch_select(B, P, O, seed, 0u, gen, nullptr, parents, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_set_profiling(mv_engine* e, int32_t enabled) {
+  if (!e) return fail(MV_ERR_ARG, "null engine");
+  e->profiling = enabled != 0;
+  return MV_OK;
+}
+
+static int ensure_events(std::vector<hipEvent_t>& v, size_t n) {
+  while (v.size() < n) {
+    hipEvent_t ev;
+    HIPCHK(hipEventCreate(&ev));
+    v.push_back(ev);
+  }
+  return MV_OK;
+}
+
+int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
+  if (!e || !prm) return fail(MV_ERR_ARG, "null argument");
+  if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  const int P = prm->pop_size, O = prm->n_offsprings, G = prm->n_gen, R = prm->n_ref;
+  if (P < 2 || O < 2 || (O & 1) || G < 1 || R < 1 || R > SURV_RMAX || P + O > SURV_NMAX ||
+      !prm->ref_points || prm->history < 0 || prm->history > 2)
+    return fail(MV_ERR_ARG,
+                "bad attack parameters (even n_offsprings, pop_size + n_offsprings <= 512, "
+                "n_ref <= 640)");
+  hipStream_t stream = (hipStream_t)stream_;
+  HIPCHK(hipSetDevice(e->device));
+  const int B = e->B, V = e->p.V, S = P + O;
+  const int hist_w = prm->history == 2 ? 3 + e->p.C : 3;
+  const int hist_rows = P + (G - 1) * O;
+  const bool realloc = !e->attack_ready || e->P != P || e->O != O || e->R != R ||
+                       e->hist_mode != prm->history || e->n_gen != G;
+  if (realloc) {
+    HIPCHK(hipDeviceSynchronize());
+    e->free_list(e->attack_allocs);
+    hipError_t err = hipSuccess;
+    auto A = [&](auto** dst, size_t n) {
+      if (err != hipSuccess) return;
+      err = dalloc(dst, n);
+      if (err == hipSuccess) e->attack_allocs.push_back((void*)*dst);
+    };
+    A(&e->pool, (size_t)B * S * V);
+    A(&e->poolF, (size_t)B * S * 3);
+    A(&e->pop_slot, (size_t)B * P);
+    A(&e->free_slot, (size_t)B * O);
+    A(&e->parents, (size_t)B * O);
+    A(&e->ideal, (size_t)B * 3);
+    A(&e->worst, (size_t)B * 3);
+    A(&e->extreme, (size_t)B * 9);
+    A(&e->has_ext, (size_t)B);
+    A(&e->ref, (size_t)R * 3);
+    if (prm->history) A(&e->hist, (size_t)B * hist_rows * hist_w);
+    if (err != hipSuccess)
+      return fail(MV_ERR_HIP, std::string("attack alloc: ") + hipGetErrorString(err));
+    e->P = P;
+    e->O = O;
+    e->S = S;
+    e->R = R;
+    e->n_gen = G;
+    e->hist_mode = prm->history;
+    e->hist_w = hist_w;
+    e->hist_rows = hist_rows;
+    e->attack_ready = true;
+  }
+  HIPCHK(hipMemcpy(e->ref, prm->ref_points, (size_t)R * 3 * sizeof(double),
+                   hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_fill_d, dim3(64), dim3(256), 0, stream, e->ideal, (size_t)B * 3,
+                     (double)INFINITY);
+  hipLaunchKernelGGL(k_fill_d, dim3(64), dim3(256), 0, stream, e->worst, (size_t)B * 3,
+                     (double)-INFINITY);
+  hipLaunchKernelGGL(k_fill_i, dim3(64), dim3(256), 0, stream, e->has_ext, (size_t)B, 0);
+  HIPCHK(hipGetLastError());
+  HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
+  // initial population evaluation (pymoo _initialize)
+  RowsArgs ev = base_rows(e);
+  ev.n = P;
+  ev.total = B * P;
+  ev.mode = 0;
+  ev.genes_in = e->pool;
+  ev.in_rows = S;
+  ev.out_rows = S;
+  ev.F = e->poolF;
+  ev.hist = prm->history ? e->hist : nullptr;
+  ev.hist_rows = hist_rows;
+  ev.hist_w = hist_w;
+  ev.hist_row0 = 0;
+  HIPCHK(launch_rows(ev, stream));
+  SurvArgs sa{};
+  sa.n_survive = P;
+  sa.P = P;
+  sa.O = O;
+  sa.F = e->poolF;
+  sa.S = S;
+  sa.pop_slot = e->pop_slot;
+  sa.free_slot = e->free_slot;
+  sa.pop_slot_out = e->pop_slot;
+  sa.ref = e->ref;
+  sa.R = R;
+  sa.mu = prm->mu;
+  sa.seed = prm->seed;
+  sa.ideal = e->ideal;
+  sa.worst = e->worst;
+  sa.extreme = e->extreme;
+  sa.has_extreme = e->has_ext;
+  sa.O_next = O;
+  // dummy survival at initialisation: n_survive == len(pop)
+  sa.N = P;
+  sa.gen = 0;
+  sa.parents_out = G > 1 ? e->parents : nullptr;
+  sa.sel_gen = 1;
+  HIPCHK(launch_survive(sa, B, stream));
+  if (e->profiling) {
+    if (ensure_events(e->ev_var, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
+    if (ensure_events(e->ev_surv, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
+  }
+  e->n_var_rec = 0;
+  e->n_surv_rec = 0;
+  RowsArgs va = base_rows(e);
+  va.n = O;
+  va.total = B * O;
+  va.mode = 1;
+  va.genes_in = e->pool;
+  va.in_rows = S;
+  va.parents = e->parents;
+  va.genes_out = e->pool;
+  va.out_rows = S;
+  va.out_map = e->free_slot;
+  va.F = e->poolF;
+  va.hist = prm->history ? e->hist : nullptr;
+  va.hist_rows = hist_rows;
+  va.hist_w = hist_w;
+  va.seed = prm->seed;
+  sa.N = P + O;
+  for (int g = 1; g < G; ++g) {
+    va.gen = g;
+    va.hist_row0 = P + (g - 1) * O;
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], stream));
+    HIPCHK(launch_rows(va, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec++ + 1], stream));
+    sa.gen = g;
+    sa.parents_out = g + 1 < G ? e->parents : nullptr;
+    sa.sel_gen = g + 1;
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec], stream));
+    HIPCHK(launch_survive(sa, B, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec++ + 1], stream));
+  }
+  return MV_OK;
+}
+
+int mv_get_kernel_times(mv_engine* e, double* vareval_ms, double* survive_ms, int32_t* n_vareval,
+                        int32_t* n_survive) {
+  if (!e) return fail(MV_ERR_ARG, "null engine");
+  double tv = 0.0, ts = 0.0;
+  for (int i = 0; i < e->n_var_rec; ++i) {
+    float ms = 0.f;
+    HIPCHK(hipEventSynchronize(e->ev_var[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms, e->ev_var[2 * i], e->ev_var[2 * i + 1]));
+    tv += ms;
+  }
+  for (int i = 0; i < e->n_surv_rec; ++i) {
+    float ms = 0.f;
+    HIPCHK(hipEventSynchronize(e->ev_surv[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms, e->ev_surv[2 * i], e->ev_surv[2 * i + 1]));
+    ts += ms;
+  }
+  if (vareval_ms) *vareval_ms = tv;
+  if (survive_ms) *survive_ms = ts;
+  if (n_vareval) *n_vareval = e->n_var_rec;
+  if (n_survive) *n_survive = e->n_surv_rec;
+  return MV_OK;
+}
+
+struct mv_mlp {
+  int device = 0;
+  MlpArgs a{};
+  std::vector<void*> allocs;
+  ~mv_mlp() {
+    (void)hipSetDevice(device);
+    for (void* x : allocs) (void)hipFree(x);
+  }
+};
+
+int mv_mlp_create(int32_t device, const mv_model_desc* md, mv_mlp** out) {
+  if (!md || !out) return fail(MV_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (md->n_layers < 2 || md->n_layers > MAX_LAYERS) return fail(MV_ERR_ARG, "2..6 layers");
+  for (int l = 1; l < md->n_layers; ++l)
+    if (md->dims[l] % 16 != 0 || md->dims[l] > 512)
+      return fail(MV_ERR_ARG, "hidden widths must be multiples of 16 and <= 512");
+  if (md->dims[md->n_layers] < 1 || md->dims[md->n_layers] > 8)
+    return fail(MV_ERR_ARG, "output width must be 1..8");
+  HIPCHK(hipSetDevice(device));
+  mv_mlp* m = new mv_mlp();
+  m->device = device;
+  MlpArgs& a = m->a;
+  a.n_layers = md->n_layers;
+  for (int l = 0; l <= md->n_layers; ++l) a.dims[l] = md->dims[l];
+  a.D4 = (md->dims[0] + 3) & ~3;
+  int hmax = 16;
+  for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
+  if (eval_region1_bytes(a.D4, hmax) + (size_t)EVAL_TR * (hmax + 1) * 4 > 160 * 1024) {
+    delete m;
+    return fail(MV_ERR_ARG, "model input too wide for the LDS tile");
+  }
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err != hipSuccess) return;
+    err = upload(dst, host, n);
+    if (err == hipSuccess) m->allocs.push_back((void*)*dst);
+  };
+  std::vector<float> w0((size_t)a.D4 * a.dims[1], 0.f);
+  std::memcpy(w0.data(), md->W[0], (size_t)a.dims[0] * a.dims[1] * sizeof(float));
+  K((float**)&a.W[0], w0.data(), w0.size());
+  K((float**)&a.bias[0], md->b[0], a.dims[1]);
+  for (int l = 1; l < a.n_layers; ++l) {
+    K((float**)&a.W[l], md->W[l], (size_t)a.dims[l] * a.dims[l + 1]);
+    K((float**)&a.bias[l], md->b[l], a.dims[l + 1]);
+  }
+  if (err != hipSuccess) {
+    delete m;
+    return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
+  }
+  *out = m;
+  return MV_OK;
+}
+
+void mv_mlp_destroy(mv_mlp* m) { delete m; }
+
+int mv_mlp_predict(mv_mlp* m, int32_t n, const double* x, double* proba, void* stream) {
+  if (!m || n < 0 || (n > 0 && (!x || !proba))) return fail(MV_ERR_ARG, "bad mv_mlp_predict");
+  HIPCHK(hipSetDevice(m->device));
+  MlpArgs a = m->a;
+  a.n = n;
+  a.x = x;
+  a.proba = proba;
+  HIPCHK(launch_predict(a, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
+  if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(launch_gather_pop(e->B, e->P, e->p.V, e->S, e->pop_slot, e->pool, e->poolF, genes, F,
+                           (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_attack_history(mv_engine* e, double* hist, void* stream) {
+  if (!e || !e->attack_ready || !e->hist_mode) return fail(MV_ERR_STATE, "no history recorded");
+  if (!hist) return fail(MV_ERR_ARG, "null hist");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(hipMemcpyAsync(hist, e->hist, (size_t)e->B * e->hist_rows * e->hist_w * sizeof(double),
+                        hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MV_OK;
+}
+
+}  // extern "C"

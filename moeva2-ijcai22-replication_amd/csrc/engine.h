@@ -1,0 +1,135 @@
+// Internal device-side layouts of the MoEvA2 engine (not part of the C ABI).
+//
+// HBM layout (all per-state arrays are state-major so a state's rows are contiguous):
+//   problem constants  : gene tables, feature maps, ML scaler, constraint program, MLP weights
+//   per-state constants: x_init[B][D], genetic bounds gl/gu[B][V], encoder MinMax over the
+//                        mutable features enc_scale/enc_min/x0_mm[B][Dm], folded layer-1
+//                        bias bias1[B][H1] (b1 + W1[immutable rows] . x_ml[immutable])
+//   population pool    : genes[B][S][V] fp64, F[B][S][3] fp64, S = P + O slots per state;
+//                        pop_slot[B][P] (population order -> slot), free_slot[B][O];
+//                        survival selects P of the P+O merged rows and the O losers'
+//                        slots receive the next offspring, so genes never move.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mv {
+
+constexpr int MAX_LAYERS = 6;
+constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
+constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
+constexpr int SURV_T = 256;      // threads per survival workgroup
+constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS
+constexpr int SURV_RMAX = 640;   // reference points
+constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound widening
+
+struct DProblem {
+  int D, V, Dm, Dm4, C, n_ohe;
+  int n_sub[2];           // crossover subsets: 0 real, 1 int (OHE genes are int)
+  const int* gene_kind;   // [V]
+  const int* gene_feat;   // [V]
+  const int* gene_sub;    // [V] index within its subset
+  const int* ohe_off;     // [n_ohe+1]
+  const int* ohe_feat;
+  const int* mut_feat;    // [Dm]
+  const double* ml_scale; // [D]
+  const double* ml_min;   // [D]
+  const int* op_code;     // [C]
+  const int* op_arg;      // [C*4]
+  const double* op_k;     // [C*2]
+  const int* idx_pool;
+  double tol;
+  int norm;               // 2 or 0 (inf)
+  int scale_obj;
+  double f2_scale;        // 1/sqrt(D) for L2, 1 for Linf
+  // classifier
+  int n_layers;
+  int dims[MAX_LAYERS + 1];
+  const float* W[MAX_LAYERS];     // W[0]: mutable rows only, [Dm4][dims[1]] zero-padded
+  const float* bias[MAX_LAYERS];  // bias[0] unused at run time (folded per state)
+};
+
+struct DStates {
+  int B;
+  const double* x_init;     // [B][D]
+  const double* gl;         // [B][V]
+  const double* gu;         // [B][V]
+  const double* enc_scale;  // [B][Dm]
+  const double* enc_min;    // [B][Dm]
+  const double* x0_mm;      // [B][Dm]
+  const float* bias1;       // [B][H1]
+  const int* min_class;     // [B]
+};
+
+// Row-tile evaluation (optionally preceded by variation) -----------------------------
+struct RowsArgs {
+  DProblem p;
+  DStates s;
+  int n;                    // rows per state
+  int total;                // B * n
+  int mode;                 // 0: genes given; 1: crossover + mutation from parents
+  const double* genes_in;   // mode 0: [B][in_rows][V]; mode 1: parent pool [B][in_rows][V]
+  int in_rows;              // rows per state in genes_in
+  const int* parents;       // mode 1: [B][n/2][2] row indices into genes_in
+  double* genes_out;        // [B][out_rows][V] or NULL
+  int out_rows;
+  const int* out_map;       // [B][n] destination row per evaluated row (NULL: identity)
+  double* F;                // [B][out_rows][3] (rows follow out_map) or NULL
+  double* G;                // [B][n][C] or NULL
+  double* hist;             // [B][hist_rows][hist_w] or NULL
+  int hist_rows, hist_w, hist_row0;
+  uint64_t seed;
+  int gen;
+  uint32_t stream_key;
+  uint32_t mut_thr;         // floor(2^32 / V)
+  double eta;               // 20
+  double cx_prob;           // 0.9
+  int do_eval;              // 0: variation only
+};
+
+// Survival ------------------------------------------------------------------------------
+struct SurvArgs {
+  int N;                    // merged individuals
+  int n_survive;
+  int P;                    // population part of the merge (slot mode)
+  int O;                    // offspring part (slot mode)
+  const double* F;          // dense: [B][N][3]; slot mode: pool F [B][S][3]
+  int S;                    // slots per state (slot mode)
+  const int* pop_slot;      // slot mode: [B][P]   (NULL -> dense mode)
+  int* free_slot;           // slot mode: [B][O]   (read, then rewritten)
+  int* pop_slot_out;        // slot mode: [B][n_survive]
+  const double* ref;        // [R][3]
+  int R;
+  double mu;
+  uint64_t seed;
+  int gen;
+  uint32_t stream_key;
+  double* ideal;            // [B][3]
+  double* worst;            // [B][3]
+  double* extreme;          // [B][9]
+  int* has_extreme;         // [B]
+  int* survivors;           // dense: [B][n_survive] merged indices
+  int* rank;                // [B][N]
+  int* order;               // [B][N]
+  int* n_ranked;            // [B]
+  int* niche;               // [B][N]
+  double* dist;             // [B][N]
+  double* nadir;            // [B][3]
+  int* parents_out;         // [B][n_m][2] (slots in slot mode, positions otherwise) or NULL
+  int O_next;               // offspring of the next generation (selection)
+  int sel_gen;
+};
+
+// Stand-alone classifier forward (Classifier.predict_proba) -------------------------------
+struct MlpArgs {
+  int n_layers;
+  int dims[MAX_LAYERS + 1];
+  const float* W[MAX_LAYERS];     // W[0] zero-padded to D4 rows
+  const float* bias[MAX_LAYERS];
+  int D4;
+  int n;
+  const double* x;                // [n][D] ML-scaled rows
+  double* proba;                  // [n][n_out]
+};
+
+}  // namespace mv

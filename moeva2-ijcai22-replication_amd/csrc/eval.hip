@@ -1,0 +1,706 @@
+// Fitness evaluation and variation kernels (gfx950).
+//
+// k_rows: one workgroup = 32 candidate rows (flattened over (state, row)), 4 waves.
+//   Phase A (one wave per row, 8 rows per wave):
+//     [mode 1] two-point crossover + polynomial mutation of the row's parents
+//              (moeva2.py:90-111 -> softmax_crossover.py:17-38 / softmax_mutation.py:20-67
+//              semantics, Philox draws), child written to the population pool;
+//     decode genes -> ML row x_f in LDS (feature_encoder.py:91-124),
+//     encoder MinMax distance f2 (default_problem.py:80-91, utils.py:11-22),
+//     ML-scaled fp32 A-tile row (default_problem.py:119-121),
+//     constraint program -> G, f3 (default_problem.py:93-97,128-129).
+//   Phase B: Dense-ReLU chain on MFMA (v_mfma_f32_16x16x4_f32, exact fp32 fma chains),
+//     layer 1 over the mutable columns only (immutable columns folded into a per-state
+//     bias), final Dense + softmax on the VALU (classifier.py:23-29).
+//   Phase C: F row (f1, f2, f3) + optional history row.
+// k_variation: phase A gene generation only (C-ABI mv_variation).
+// k_setup_states: per-state constants (mv_set_states).
+#include "engine.h"
+#include "kernels.h"
+#include "philox.h"
+
+namespace mv {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double nanmax(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return b > a ? b : a;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nanmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// numpy float remainder (npy_divmod): result takes the divisor's sign
+__device__ __forceinline__ double py_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0.0) != (m < 0.0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+__device__ __forceinline__ double month_of(double f) {
+  return floor(f / 100.0) * 12.0 + py_mod(f, 100.0);
+}
+
+// One constraint column on the ML row x (LDS).
+__device__ double eval_op(const DProblem& p, int c, const double* __restrict__ x) {
+  const int code = p.op_code[c];
+  const int* ar = p.op_arg + 4 * c;
+  const double* k = p.op_k + 2 * c;
+  switch (code) {
+    case 1:  // MV_OP_DIFF
+      return x[ar[0]] - x[ar[1]];
+    case 2: {  // MV_OP_RATIO_SAFE
+      const double a = x[ar[0]], b = x[ar[1]];
+      return (b != 0.0 ? a / b : 0.0) - k[0];
+    }
+    case 3: {  // MV_OP_ABS_SUMDIFF (integer-valued features in every shipped program)
+      double s0 = 0.0, s1 = 0.0;
+      for (int q = ar[0]; q < ar[1]; ++q) s0 += x[p.idx_pool[q]];
+      for (int q = ar[1]; q < ar[2]; ++q) s1 += x[p.idx_pool[q]];
+      return fabs(s0 - s1);
+    }
+    case 4: {  // MV_OP_LCLD_INSTALL (lcld_constraints.py:174-177), numpy evaluation order
+      const double x0 = x[ar[0]], x1 = x[ar[1]], x2 = x[ar[2]], x3 = x[ar[3]];
+      const double r = x2 / 1200.0;
+      const double base = 1.0 + x2 / 1200.0;
+      const double num = (x0 * r) * pow(base, x1);
+      const double den = pow(base, x1) - 1.0;
+      return fabs(x3 - num / den) - k[0];
+    }
+    case 5: {  // MV_OP_LCLD_TERM
+      const double t = x[ar[0]];
+      return fabs((36.0 - t) * (60.0 - t));
+    }
+    case 6:  // MV_OP_ABS_RATIO
+      return fabs(x[ar[0]] - x[ar[1]] / x[ar[2]]);
+    case 7:  // MV_OP_MONTHDIFF
+      return fabs(x[ar[0]] - (month_of(x[ar[1]]) - month_of(x[ar[2]])));
+    case 8: {  // MV_OP_RATIO_MASKED
+      const double den = x[ar[2]];
+      double ratio = -1.0;
+      if (den != 0.0) {
+        ratio = x[ar[1]] / den;
+        if (ratio == __builtin_inf() || ratio != ratio) ratio = -1.0;
+      }
+      return fabs(x[ar[0]] - ratio);
+    }
+    case 9: {  // MV_OP_XOR_AUG
+      const bool b1 = x[ar[1]] >= k[0];
+      const bool b2 = x[ar[2]] >= k[1];
+      return fabs(x[ar[0]] - ((b1 != b2) ? 1.0 : 0.0));
+    }
+    default:
+      return __builtin_nan("");
+  }
+}
+
+// pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction.
+__device__ __forceinline__ double poly_mut(double x, double xl, double xu, double u, double eta) {
+  const double d1 = (x - xl) / (xu - xl);
+  const double d2 = (xu - x) / (xu - xl);
+  const double mp = 1.0 / (eta + 1.0);
+  double dq;
+  if (u <= 0.5) {
+    const double xy = 1.0 - d1;
+    const double val = 2.0 * u + (1.0 - 2.0 * u) * pow(xy, eta + 1.0);
+    dq = pow(val, mp) - 1.0;
+  } else {
+    const double xy = 1.0 - d2;
+    const double val = 2.0 * (1.0 - u) + 2.0 * (u - 0.5) * pow(xy, eta + 1.0);
+    dq = 1.0 - pow(val, mp);
+  }
+  double y = x + dq * (xu - xl);
+  if (y < xl) y = xl;
+  if (y > xu) y = xu;
+  return y;
+}
+
+struct Cx {
+  int on[2];
+  int lo[2];
+  int hi[2];
+};
+
+// Crossover draws of mating m for both variable-type subsets (oracle crossover_draws).
+__device__ __forceinline__ Cx cx_draws(const Rng& rng, int gen, int m, const int n_sub[2],
+                                       double prob) {
+  Cx c;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int n = n_sub[s];
+    c.on[s] = 0;
+    c.lo[s] = 0;
+    c.hi[s] = 0;
+    if (n <= 0) continue;
+    const u32x4 w = rng.draw((uint32_t)(m * 2 + s), (uint32_t)gen, TAG_CX);
+    c.on[s] = u53(w.x, w.y) < prob;
+    if (n - 1 <= 0) continue;
+    const int a = 1 + (int)(((uint64_t)w.z * (uint64_t)(n - 1)) >> 32);
+    if (n - 1 == 1) {
+      c.lo[s] = a;
+      c.hi[s] = n;
+    } else {
+      int b = 1 + (int)(((uint64_t)w.w * (uint64_t)(n - 2)) >> 32);
+      if (b >= a) ++b;
+      c.lo[s] = a < b ? a : b;
+      c.hi[s] = a < b ? b : a;
+    }
+  }
+  return c;
+}
+
+// Child gene g of offspring i (parents own/oth), crossover + mutation.
+__device__ __forceinline__ double child_gene(const RowsArgs& a, const Rng& rng, const Cx& cx,
+                                             const double* __restrict__ gown,
+                                             const double* __restrict__ goth, int b, int i, int g,
+                                             uint32_t word) {
+  const DProblem& p = a.p;
+  const int kind = p.gene_kind[g];
+  const int ss = kind == 0 ? 0 : 1;
+  const int sub = p.gene_sub[g];
+  const bool swap = cx.on[ss] && sub >= cx.lo[ss] && sub < cx.hi[ss];
+  double x = swap ? goth[g] : gown[g];
+  if (word < a.mut_thr) {
+    const u32x4 wu = rng.draw((uint32_t)(i * p.V + g), (uint32_t)a.gen, TAG_MUT_U);
+    const double u = u53(wu.x, wu.y);
+    const double xl = a.s.gl[(size_t)b * p.V + g];
+    const double xu = a.s.gu[(size_t)b * p.V + g];
+    if (kind == 0) {
+      x = poly_mut(x, xl, xu, u, a.eta);
+    } else {
+      double y = poly_mut(x, xl - INT_WIDEN, xu + INT_WIDEN, u, a.eta);
+      y = rint(y);  // np.round: half to even
+      if (y < xl) y = xl;
+      if (y > xu) y = xu;
+      x = y;
+    }
+  }
+  return x;
+}
+
+__device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restrict__ xrow, int g,
+                                             double x) {
+  if (p.gene_kind[g] != 2) {
+    xrow[p.gene_feat[g]] = x;
+  } else {
+    const int q = p.gene_feat[g];
+    const int o0 = p.ohe_off[q], o1 = p.ohe_off[q + 1];
+    for (int k = o0; k < o1; ++k) xrow[p.ohe_feat[k]] = (x == (double)(k - o0)) ? 1.0 : 0.0;
+  }
+}
+
+// Generate (mode 1) or load (mode 0) the genes of row (b, i); lane-parallel, 4 genes/lane.
+__device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xrow) {
+  const DProblem& p = a.p;
+  const int V = p.V;
+  double* gout = nullptr;
+  if (a.genes_out) {
+    const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
+    gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
+  }
+  if (a.mode == 0) {
+    const double* gin = a.genes_in + ((size_t)b * a.in_rows + i) * V;
+    for (int g = lane; g < V; g += 64) {
+      const double x = gin[g];
+      if (gout) gout[g] = x;
+      if (xrow) scatter_gene(p, xrow, g, x);
+    }
+    return;
+  }
+  const Rng rng(a.seed, a.stream_key);
+  const int nm = a.n / 2;
+  const int m = i % nm;
+  const int side = i / nm;
+  const int* par = a.parents + ((size_t)b * nm + m) * 2;
+  const int own = side ? par[1] : par[0];
+  const int oth = side ? par[0] : par[1];
+  const double* gown = a.genes_in + ((size_t)b * a.in_rows + own) * V;
+  const double* goth = a.genes_in + ((size_t)b * a.in_rows + oth) * V;
+  const Cx cx = cx_draws(rng, a.gen, m, p.n_sub, a.cx_prob);
+  const int nq = (V + 3) >> 2;
+  for (int g0 = lane * 4; g0 < V; g0 += 256) {
+    const u32x4 w = rng.draw((uint32_t)(i * nq + (g0 >> 2)), (uint32_t)a.gen, TAG_MUT_MASK);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int g = g0 + j;
+      if (g < V) {
+        const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
+        const double x = child_gene(a, rng, cx, gown, goth, b, i, g, word);
+        if (gout) gout[g] = x;
+        if (xrow) scatter_gene(p, xrow, g, x);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Dense layer on MFMA: out[32][N] = relu(in[32][K] . W[K][N] + bias), K % 4 == 0, N % 16 == 0.
+template <int MAXCT>
+__device__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
+                           const float* __restrict__ W, int N, const float* __restrict__ bias,
+                           const float* __restrict__ bias_state, const int* row_state,
+                           float* __restrict__ out, int ldo, int wave, int lane) {
+  const int nct = N >> 4;
+  floatx4 acc[2][MAXCT];
+#pragma unroll
+  for (int c = 0; c < MAXCT; ++c) {
+    acc[0][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ka = lane >> 4;
+  const int il = lane & 15;
+  const float* in0 = in + il * ldi + ka;
+  const float* in1 = in + (il + 16) * ldi + ka;
+#pragma unroll 4
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const float a0 = in0[k0];
+    const float a1 = in1[k0];
+    const float* wr = W + (size_t)(k0 + ka) * N + il;
+#pragma unroll
+    for (int c = 0; c < MAXCT; ++c) {
+      const int ct = wave + c * 4;
+      if (ct < nct) {
+        const float bf = wr[ct * 16];
+        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf, acc[0][c], 0, 0, 0);
+        acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf, acc[1][c], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < MAXCT; ++c) {
+    const int ct = wave + c * 4;
+    if (ct < nct) {
+      const int col = ct * 16 + il;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = rt * 16 + ka * 4 + j;
+          float bv;
+          if (bias_state) {
+            const int st = row_state[row] < 0 ? 0 : row_state[row];
+            bv = bias_state[(size_t)st * N + col];
+          } else {
+            bv = bias[col];
+          }
+          float v = acc[rt][c][j] + bv;
+          out[row * ldo + col] = v > 0.f ? v : 0.f;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int max_hidden(const DProblem& p) {
+  int h = 16;
+  for (int l = 1; l < p.n_layers; ++l) h = p.dims[l] > h ? p.dims[l] : h;
+  return h;
+}
+
+template <int MAXCT>
+__global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int lda = p.Dm4 + 1;
+  const int hmax = max_hidden(p);
+  // LDS carve (kept in sync with eval_lds_bytes)
+  int* row_state = (int*)smem;                       // [32]
+  int* row_idx = row_state + EVAL_TR;                // [32]
+  double* row_f2 = (double*)(row_idx + EVAL_TR);     // [32]
+  double* row_f3 = row_f2 + EVAL_TR;                 // [32]
+  unsigned char* base = (unsigned char*)(row_f3 + EVAL_TR);
+  const size_t r1 = eval_region1_bytes(p.Dm4, hmax);
+  float* R1 = (float*)base;
+  unsigned char* R2 = base + r1;
+  const int r0 = blockIdx.x * EVAL_TR;
+
+  // ---------------- Phase A
+  for (int rr = 0; rr < EVAL_TR / 4; ++rr) {
+    const int t = rr * 4 + wave;
+    const int r = r0 + t;
+    const bool valid = r < a.total;
+    double* xrow = (double*)R2 + (size_t)wave * p.D;
+    int b = 0, i = 0;
+    if (valid) {
+      b = r / a.n;
+      i = r - b * a.n;
+      const double* xi = a.s.x_init + (size_t)b * p.D;
+      for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
+    }
+    __syncthreads();
+    if (valid) row_genes(a, b, i, lane, xrow);
+    __syncthreads();
+    float* arow = R1 + t * lda;
+    if (valid) {
+      const double* es = a.s.enc_scale + (size_t)b * p.Dm;
+      const double* em = a.s.enc_min + (size_t)b * p.Dm;
+      const double* x0 = a.s.x0_mm + (size_t)b * p.Dm;
+      double acc = 0.0;
+      for (int j = lane; j < p.Dm4; j += 64) {
+        float v = 0.f;
+        if (j < p.Dm) {
+          const int f = p.mut_feat[j];
+          const double xf = xrow[f];
+          const double xm = xf * p.ml_scale[f] + p.ml_min[f];
+          v = (float)xm;
+          const double mm = xf * es[j] + em[j];
+          const double d = mm - x0[j];
+          if (p.norm == 2)
+            acc += d * d;
+          else
+            acc = nanmax(acc, fabs(d));
+        }
+        arow[j] = v;
+      }
+      acc = p.norm == 2 ? wave_sum(acc) : wave_max(acc);
+      double f2 = p.norm == 2 ? sqrt(acc) : acc;
+      if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
+      double acc3 = 0.0;
+      double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+      double* hrow = (a.hist && a.hist_w > 3)
+                         ? a.hist + ((size_t)b * a.hist_rows + a.hist_row0 + i) * a.hist_w + 3
+                         : nullptr;
+      for (int c = lane; c < p.C; c += 64) {
+        double v = eval_op(p, c, xrow);
+        if (v <= p.tol) v = 0.0;
+        const double g = v * (v > 0.0 ? 1.0 : 0.0);
+        if (grow) grow[c] = g;
+        if (hrow) hrow[c] = g;
+        acc3 += g;
+      }
+      acc3 = wave_sum(acc3);
+      if (lane == 0) {
+        row_state[t] = b;
+        row_idx[t] = i;
+        row_f2[t] = f2;
+        row_f3[t] = acc3;
+      }
+    } else {
+      for (int j = lane; j < p.Dm4; j += 64) arow[j] = 0.f;
+      if (lane == 0) {
+        row_state[t] = -1;
+        row_idx[t] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (!a.do_eval) return;
+
+  // ---------------- Phase B: Dense chain
+  const float* in = R1;
+  int ldi = lda;
+  int K = p.Dm4;
+  float* outb = (float*)R2;
+  float* other = R1;
+  for (int l = 0; l + 1 < p.n_layers; ++l) {
+    const int N = p.dims[l + 1];
+    const int ldo = N + 1;
+    dense_mfma<MAXCT>(in, ldi, K, p.W[l], N, p.bias[l], l == 0 ? a.s.bias1 : nullptr, row_state,
+                      outb, ldo, wave, lane);
+    __syncthreads();
+    in = outb;
+    ldi = ldo;
+    K = N;
+    float* tmp = outb;
+    outb = other;
+    other = tmp;
+  }
+  // final Dense + softmax (VALU), one thread per row
+  if (tid < EVAL_TR) {
+    const int t = tid;
+    const int st = row_state[t];
+    if (st >= 0) {
+      const int L = p.n_layers - 1;
+      const int nout = p.dims[L + 1];
+      const float* Wl = p.W[L];
+      const float* bl = p.bias[L];
+      float logit[8];
+      float mx = -__builtin_inff();
+      for (int c = 0; c < nout; ++c) {
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], Wl[(size_t)k * nout + c], s);
+        logit[c] = s + bl[c];
+        mx = logit[c] > mx ? logit[c] : mx;
+      }
+      float den = 0.f;
+      for (int c = 0; c < nout; ++c) {
+        logit[c] = expf(logit[c] - mx);
+        den += logit[c];
+      }
+      const int mc = a.s.min_class[st];
+      const double f1 = (double)(logit[mc] / den);
+      const int i = row_idx[t];
+      if (a.F) {
+        const int orow = a.out_map ? a.out_map[(size_t)st * a.n + i] : i;
+        double* fr = a.F + ((size_t)st * a.out_rows + orow) * 3;
+        fr[0] = f1;
+        fr[1] = row_f2[t];
+        fr[2] = row_f3[t];
+      }
+      if (a.hist) {
+        double* hr = a.hist + ((size_t)st * a.hist_rows + a.hist_row0 + i) * a.hist_w;
+        hr[0] = f1;
+        hr[1] = row_f2[t];
+        hr[2] = row_f3[t];
+      }
+    }
+  }
+}
+
+// Classifier.predict_proba: 32 rows per workgroup, full-width first layer.
+template <int MAXCT>
+__global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int hmax = 16;
+  for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
+  const int lda = a.D4 + 1;
+  const size_t r1 = eval_region1_bytes(a.D4, hmax);
+  float* R1 = (float*)smem;
+  float* R2 = (float*)(smem + r1);
+  const int D = a.dims[0];
+  const int r0 = blockIdx.x * EVAL_TR;
+  for (int idx = tid; idx < EVAL_TR * a.D4; idx += EVAL_T) {
+    const int t = idx / a.D4, j = idx - t * a.D4;
+    const int r = r0 + t;
+    R1[t * lda + j] = (r < a.n && j < D) ? (float)a.x[(size_t)r * D + j] : 0.f;
+  }
+  __syncthreads();
+  const float* in = R1;
+  int ldi = lda, K = a.D4;
+  float* outb = R2;
+  float* other = R1;
+  for (int l = 0; l + 1 < a.n_layers; ++l) {
+    const int N = a.dims[l + 1];
+    dense_mfma<MAXCT>(in, ldi, K, a.W[l], N, a.bias[l], nullptr, nullptr, outb, N + 1, wave,
+                      lane);
+    __syncthreads();
+    in = outb;
+    ldi = N + 1;
+    K = N;
+    float* tmp = outb;
+    outb = other;
+    other = tmp;
+  }
+  if (tid < EVAL_TR && r0 + tid < a.n) {
+    const int t = tid;
+    const int L = a.n_layers - 1;
+    const int nout = a.dims[L + 1];
+    float logit[8];
+    float mx = -__builtin_inff();
+    for (int c = 0; c < nout; ++c) {
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], a.W[L][(size_t)k * nout + c], s);
+      logit[c] = s + a.bias[L][c];
+      mx = logit[c] > mx ? logit[c] : mx;
+    }
+    float den = 0.f;
+    for (int c = 0; c < nout; ++c) {
+      logit[c] = expf(logit[c] - mx);
+      den += logit[c];
+    }
+    for (int c = 0; c < nout; ++c) a.proba[(size_t)(r0 + t) * nout + c] = (double)(logit[c] / den);
+  }
+}
+
+// Constraints only (Constraints.evaluate numpy path): one wave per ML-space row.
+__global__ __launch_bounds__(256) void k_constraints(DProblem p, int n, const double* x, double* G) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wave;
+  double* xrow = (double*)smem + (size_t)wave * p.D;
+  if (r < n)
+    for (int f = lane; f < p.D; f += 64) xrow[f] = x[(size_t)r * p.D + f];
+  __syncthreads();
+  if (r >= n) return;
+  for (int c = lane; c < p.C; c += 64) {
+    double v = eval_op(p, c, xrow);
+    if (v <= p.tol) v = 0.0;
+    G[(size_t)r * p.C + c] = v;
+  }
+}
+
+// Variation only: one wave per offspring row.
+__global__ __launch_bounds__(256) void k_variation(RowsArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.total) return;
+  const int b = r / a.n;
+  const int i = r - b * a.n;
+  row_genes(a, b, i, lane, nullptr);
+}
+
+// Per-state constants: one workgroup per state.
+__global__ __launch_bounds__(256) void k_setup_states(DProblem p, int B, const double* x_init,
+                                                      const double* xl, const double* xu,
+                                                      const float* W1full, const float* b1,
+                                                      double* gl, double* gu, double* enc_scale,
+                                                      double* enc_min, double* x0_mm,
+                                                      float* bias1, double* genes0) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const double* xi = x_init + (size_t)b * p.D;
+  const double* lo = xl + (size_t)b * p.D;
+  const double* hi = xu + (size_t)b * p.D;
+  for (int g = tid; g < p.V; g += blockDim.x) {
+    const int kind = p.gene_kind[g];
+    double l, u, x0;
+    if (kind != 2) {
+      const int f = p.gene_feat[g];
+      l = lo[f];
+      u = hi[f];
+      x0 = xi[f];
+      if (kind != 0) x0 = rint(x0);  // sampling.py:74-76
+    } else {
+      const int q = p.gene_feat[g];
+      const int o0 = p.ohe_off[q], o1 = p.ohe_off[q + 1];
+      l = 0.0;
+      u = (double)(o1 - o0 - 1);
+      int best = 0;
+      double bv = xi[p.ohe_feat[o0]];
+      for (int k = o0 + 1; k < o1; ++k) {  // OneHotEncoder.inverse_transform = argmax
+        const double v = xi[p.ohe_feat[k]];
+        if (v > bv) {
+          bv = v;
+          best = k - o0;
+        }
+      }
+      x0 = (double)best;
+    }
+    gl[(size_t)b * p.V + g] = l;
+    gu[(size_t)b * p.V + g] = u;
+    genes0[(size_t)b * p.V + g] = x0;
+  }
+  for (int j = tid; j < p.Dm; j += blockDim.x) {
+    const int f = p.mut_feat[j];
+    const double a0 = lo[f], a1 = hi[f];
+    const double mn = a0 < a1 ? a0 : a1;
+    const double mx = a0 < a1 ? a1 : a0;
+    double rng = mx - mn;
+    if (rng == 0.0) rng = 1.0;
+    const double sc = 1.0 / rng;
+    const double mi = 0.0 - mn * sc;
+    enc_scale[(size_t)b * p.Dm + j] = sc;
+    enc_min[(size_t)b * p.Dm + j] = mi;
+    x0_mm[(size_t)b * p.Dm + j] = xi[f] * sc + mi;
+  }
+  // layer-1 bias fold over the immutable features (fp32, Keras casts inputs to float32)
+  const int H1 = p.dims[1];
+  for (int h = tid; h < H1; h += blockDim.x) {
+    float s = 0.f;
+    int jm = 0;
+    for (int f = 0; f < p.D; ++f) {
+      if (jm < p.Dm && p.mut_feat[jm] == f) {
+        ++jm;
+        continue;
+      }
+      const float xv = (float)(xi[f] * p.ml_scale[f] + p.ml_min[f]);
+      s = fmaf(xv, W1full[(size_t)f * H1 + h], s);
+    }
+    bias1[(size_t)b * H1 + h] = b1[h] + s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Allow up to the full 160 KiB of LDS per workgroup for the dynamic-LDS kernels.
+static void configure_lds_once() {
+  static bool done = false;
+  if (done) return;
+  const int lim = 160 * 1024;
+  (void)hipFuncSetAttribute((const void*)k_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_rows<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_rows<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_predict<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_predict<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_predict<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_predict<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_constraints, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipGetLastError();
+  done = true;
+}
+
+hipError_t launch_rows(const RowsArgs& a, hipStream_t stream) {
+  if (a.total <= 0) return hipSuccess;
+  configure_lds_once();
+  int hmax = 16;
+  for (int l = 1; l < a.p.n_layers; ++l) hmax = a.p.dims[l] > hmax ? a.p.dims[l] : hmax;
+  const size_t lds = eval_lds_bytes(a.p.D, a.p.Dm4, hmax);
+  const int grid = (a.total + EVAL_TR - 1) / EVAL_TR;
+  int maxn = 16;
+  for (int l = 1; l < a.p.n_layers; ++l) maxn = a.p.dims[l] > maxn ? a.p.dims[l] : maxn;
+  const int nct = maxn / 16;
+  if (nct <= 4)
+    hipLaunchKernelGGL(k_rows<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 8)
+    hipLaunchKernelGGL(k_rows<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 16)
+    hipLaunchKernelGGL(k_rows<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else
+    hipLaunchKernelGGL(k_rows<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_predict(const MlpArgs& a, hipStream_t stream) {
+  if (a.n <= 0) return hipSuccess;
+  configure_lds_once();
+  int hmax = 16;
+  for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
+  const size_t lds = eval_region1_bytes(a.D4, hmax) + (size_t)EVAL_TR * (hmax + 1) * 4;
+  const int grid = (a.n + EVAL_TR - 1) / EVAL_TR;
+  const int nct = hmax / 16;
+  if (nct <= 4)
+    hipLaunchKernelGGL(k_predict<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 8)
+    hipLaunchKernelGGL(k_predict<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 16)
+    hipLaunchKernelGGL(k_predict<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  else
+    hipLaunchKernelGGL(k_predict<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_constraints(const DProblem& p, int n, const double* x, double* G,
+                              hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  configure_lds_once();
+  hipLaunchKernelGGL(k_constraints, dim3((n + 3) / 4), dim3(256), (size_t)4 * p.D * 8, stream, p,
+                     n, x, G);
+  return hipGetLastError();
+}
+
+hipError_t launch_variation(const RowsArgs& a, hipStream_t stream) {
+  if (a.total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_variation, dim3((a.total + 3) / 4), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_setup_states(const DProblem& p, int B, const double* x_init, const double* xl,
+                               const double* xu, const float* W1full, const float* b1, double* gl,
+                               double* gu, double* enc_scale, double* enc_min, double* x0_mm,
+                               float* bias1, double* genes0, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_setup_states, dim3(B), dim3(256), 0, stream, p, B, x_init, xl, xu, W1full,
+                     b1, gl, gu, enc_scale, enc_min, x0_mm, bias1, genes0);
+  return hipGetLastError();
+}
+
+}  // namespace mv

@@ -1,0 +1,66 @@
+// Philox4x32-10 counter-based RNG for the MoEvA2 engine (gfx950).
+//
+// The reference draws from numpy's MT19937 inside pymoo, re-seeded with the same seed
+// for every initial state (src/attacks/moeva2/moeva2.py:158-165).  The engine replaces
+// that stream with Philox so every draw is a pure function of
+//     key     = (seed lo32, seed hi32)
+//     counter = (index, stream_key, generation, tag)
+// which makes results independent of the state's position, the shard and the launch
+// geometry.  oracle/philox.py states the same layout on the CPU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mv {
+
+enum : uint32_t {
+  TAG_SEL_PERM = 1,
+  TAG_SEL_CHOICE = 2,
+  TAG_CX = 3,
+  TAG_MUT_MASK = 4,
+  TAG_MUT_U = 5,
+  TAG_NICHE_PERM = 6,
+  TAG_NICHE_MEMBER = 7,
+};
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                        uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c0;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return {c0, c1, c2, c3};
+}
+
+struct Rng {
+  uint32_t k0, k1, sk;
+  __device__ __forceinline__ Rng(uint64_t seed, uint32_t stream_key)
+      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), sk(stream_key) {}
+  __device__ __forceinline__ u32x4 draw(uint32_t index, uint32_t gen, uint32_t tag) const {
+    return philox(index, sk, gen, tag, k0, k1);
+  }
+};
+
+// 53-bit uniform in [0,1): MT19937 genrand_res53 form on two Philox words.
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+}  // namespace mv

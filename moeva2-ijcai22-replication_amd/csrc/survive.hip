@@ -1,0 +1,851 @@
+// R-NSGA-III survival + tournament selection (gfx950), one workgroup per initial state.
+//
+// Restates pymoo 0.4.2.2 (not vendored; [pymoo-recall]):
+//   rnsga3.AspirationPointSurvival._do      ideal/worst, NDS, extreme points, nadir,
+//                                           aspiration ref dirs, association, niching
+//   NonDominatedSorting (fast_non_dominated_sort discovery order, n_stop_if_ranked)
+//   nsga3.get_extreme_points_c / get_nadir_point / associate_to_niches / niching
+//   TournamentSelection(comp_by_cv_then_random) (all CV == 0: random winner)
+// with the dominance relation of src/attacks/moeva2/pareto_operation.py:148-164.
+// Every floating-point expression keeps numpy's evaluation order (the library is built
+// with -ffp-contract=off) so ranks, niches and survivors are bit-identical to
+// oracle/moeva_oracle.py on identical objective arrays.
+//
+// Data: the merged population's F rows (LDS), a dominated-by bitset per individual
+// (ceil(N/64) words), fronts as an ordered index array, niche CSR for the last front.
+#include <limits.h>
+
+#include "engine.h"
+#include "kernels.h"
+#include "philox.h"
+
+namespace mv {
+
+namespace {
+
+struct SurvLds {
+  double* F;        // [N*3]
+  double* ref;      // [R*3]
+  double* U;        // [(R+3)*3] normalised reference directions
+  double* dist;     // [N]
+  double* red;      // [4*16] reduction scratch
+  double* scal;     // [32] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9)
+  unsigned long long* dom;     // [N*NW]
+  unsigned long long* ranked;  // [NW]
+  unsigned long long* cur;     // [NW]
+  int* I;           // [N] fronts concatenated
+  int* pos;         // [N] position in own front
+  int* front_of;    // [N]
+  int* slot;        // [N]
+  int* niche;       // [N]
+  int* memb;        // [N]
+  int* key;         // [N]
+  int* surv;        // [N]
+  int* sel;         // [N]
+  int* fstart;      // [N+2]
+  int* count;       // [R+3]
+  int* remain;      // [R+3]
+  int* csr_off;     // [R+4]
+  int* csr;         // [N]
+  int* cand;        // [R+3]
+  int* ckey;        // [R+3]
+  int* iscal;       // [16]
+  int* selkey;      // [n_perm_slots]
+  int* perm;        // [n_perm_slots]
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ inline size_t surv_layout(int N, int R, int Pperm, SurvLds* L, unsigned char* base) {
+  const int NW = (N + 63) / 64;
+  const int RN = R + 3;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = align16(off + bytes);
+    return o;
+  };
+  const size_t oF = take((size_t)N * 3 * 8), oRef = take((size_t)R * 3 * 8),
+               oU = take((size_t)RN * 3 * 8), oDist = take((size_t)N * 8), oRed = take(64 * 8),
+               oScal = take(32 * 8), oDom = take((size_t)N * NW * 8), oRk = take(NW * 8),
+               oCur = take(NW * 8), oI = take(N * 4), oPos = take(N * 4), oFo = take(N * 4),
+               oSlot = take(N * 4), oNi = take(N * 4), oMe = take(N * 4), oKey = take(N * 4),
+               oSurv = take(N * 4), oSel = take(N * 4), oFs = take((N + 2) * 4),
+               oCnt = take(RN * 4), oRem = take(RN * 4), oCo = take((RN + 1) * 4),
+               oCsr = take(N * 4), oCand = take(RN * 4), oCk = take(RN * 4), oIs = take(16 * 4),
+               oSk = take((size_t)Pperm * 4), oPerm = take((size_t)Pperm * 4);
+  if (L) {
+    L->F = (double*)(base + oF);
+    L->ref = (double*)(base + oRef);
+    L->U = (double*)(base + oU);
+    L->dist = (double*)(base + oDist);
+    L->red = (double*)(base + oRed);
+    L->scal = (double*)(base + oScal);
+    L->dom = (unsigned long long*)(base + oDom);
+    L->ranked = (unsigned long long*)(base + oRk);
+    L->cur = (unsigned long long*)(base + oCur);
+    L->I = (int*)(base + oI);
+    L->pos = (int*)(base + oPos);
+    L->front_of = (int*)(base + oFo);
+    L->slot = (int*)(base + oSlot);
+    L->niche = (int*)(base + oNi);
+    L->memb = (int*)(base + oMe);
+    L->key = (int*)(base + oKey);
+    L->surv = (int*)(base + oSurv);
+    L->sel = (int*)(base + oSel);
+    L->fstart = (int*)(base + oFs);
+    L->count = (int*)(base + oCnt);
+    L->remain = (int*)(base + oRem);
+    L->csr_off = (int*)(base + oCo);
+    L->csr = (int*)(base + oCsr);
+    L->cand = (int*)(base + oCand);
+    L->ckey = (int*)(base + oCk);
+    L->iscal = (int*)(base + oIs);
+    L->selkey = (int*)(base + oSk);
+    L->perm = (int*)(base + oPerm);
+  }
+  return off;
+}
+
+__device__ __forceinline__ double min_prop(double a, double b) {  // np.min (NaN propagates)
+  if (a != a) return a;
+  if (b != b) return b;
+  return b < a ? b : a;
+}
+__device__ __forceinline__ double max_prop(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return b > a ? b : a;
+}
+
+// np.argmin order: first NaN, else smallest value, ties -> smallest index
+__device__ __forceinline__ bool arg_better(double v, int i, double bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return (vn && bn) ? (i < bi) : vn;
+  return v < bv || (v == bv && i < bi);
+}
+
+__device__ __forceinline__ bool dominates(const double* a, const double* b) {
+  const bool lt = (a[0] < b[0]) | (a[1] < b[1]) | (a[2] < b[2]);
+  const bool gt = (a[0] > b[0]) | (a[1] > b[1]) | (a[2] > b[2]);
+  return lt && !gt;
+}
+
+// Ordered stream compaction of the indices i in [0, n) with pred(i) into out[base..].
+// Returns the count (uniform).  Uses red scratch as int[4+1].
+template <class Pred>
+__device__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int total = 0;
+  for (int b0 = 0; b0 < n; b0 += SURV_T) {
+    const int i = b0 + tid;
+    const bool f = i < n && pred(i);
+    const unsigned long long m = __ballot(f);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int woff = 0, all = 0;
+    for (int w = 0; w < SURV_T / 64; ++w) {
+      if (w < wave) woff += wsum[w];
+      all += wsum[w];
+    }
+    if (f) out[base + total + woff + before] = i;
+    total += all;
+    __syncthreads();
+  }
+  return total;
+}
+
+__device__ __forceinline__ double wred_min(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = min_prop(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wred_max(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = max_prop(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wred_imin(int v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// LAPACK dgetf2/dgetrs-order 3x3 solve (oracle lu_solve3).  Returns false if singular.
+__device__ bool lu_solve3(double A[3][3], double x[3]) {
+  for (int k = 0; k < 3; ++k) {
+    int p = k;
+    for (int i = k + 1; i < 3; ++i)
+      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+    if (A[p][k] == 0.0) return false;
+    if (p != k) {
+      for (int j = 0; j < 3; ++j) {
+        const double t = A[k][j];
+        A[k][j] = A[p][j];
+        A[p][j] = t;
+      }
+      const double t = x[k];
+      x[k] = x[p];
+      x[p] = t;
+    }
+    const double r = 1.0 / A[k][k];
+    for (int i = k + 1; i < 3; ++i) A[i][k] = A[i][k] * r;
+    for (int j = k + 1; j < 3; ++j)
+      for (int i = k + 1; i < 3; ++i) A[i][j] = A[i][j] - A[i][k] * A[k][j];
+  }
+  for (int j = 0; j < 3; ++j)
+    for (int i = j + 1; i < 3; ++i) x[i] = x[i] - x[j] * A[i][j];
+  for (int j = 2; j >= 0; --j) {
+    x[j] = x[j] / A[j][j];
+    for (int i = 0; i < j; ++i) x[i] = x[i] - x[j] * A[i][j];
+  }
+  return true;
+}
+
+// Tournament selection for the next generation (oracle tournament_parents).
+__device__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
+                           const int* map_slot, int* out, int* selkey, int* perm) {
+  const int tid = threadIdx.x;
+  const int n_m = (O_next + 1) / 2;
+  const int n_random = n_m * 4;
+  const int n_perms = (n_random + P - 1) / P;
+  const Rng rng(seed, sk);
+  for (int idx = tid; idx < n_perms * P; idx += SURV_T)
+    selkey[idx] = (int)rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
+  __syncthreads();
+  for (int idx = tid; idx < n_perms * P; idx += SURV_T) {
+    const int q = idx / P, i = idx - q * P;
+    const unsigned ki = (unsigned)selkey[idx];
+    int r = 0;
+    for (int j = 0; j < P; ++j) {
+      const unsigned kj = (unsigned)selkey[q * P + j];
+      r += (kj < ki) || (kj == ki && j < i);
+    }
+    perm[q * P + r] = i;
+  }
+  __syncthreads();
+  for (int t = tid; t < 2 * n_m; t += SURV_T) {
+    const int a = perm[2 * t], b = perm[2 * t + 1];
+    const unsigned bit = rng.draw((uint32_t)t, (uint32_t)gen, TAG_SEL_CHOICE).x & 1u;
+    const int w = bit ? b : a;
+    out[t] = map_slot ? map_slot[w] : w;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.N, R = a.R, RN = R + 3;
+  const int NW = (N + 63) / 64;
+  const int n_m_next = a.parents_out ? (a.O_next + 1) / 2 : 0;
+  const int pslots = a.parents_out ? ((n_m_next * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
+  SurvLds L;
+  surv_layout(N, R, pslots, &L, smem);
+  double* ideal = L.scal;
+  double* worst = L.scal + 3;
+  double* wpop = L.scal + 6;
+  double* wfront = L.scal + 9;
+  double* nadir = L.scal + 12;
+  double* ext = L.scal + 15;  // 9
+  const bool slot_mode = a.pop_slot != nullptr;
+
+  // ---- load merged F, ref points
+  for (int m = tid; m < N; m += SURV_T) {
+    int s = m;
+    const double* src;
+    if (slot_mode) {
+      s = m < a.P ? a.pop_slot[(size_t)b * a.P + m] : a.free_slot[(size_t)b * a.O + (m - a.P)];
+      src = a.F + ((size_t)b * a.S + s) * 3;
+    } else {
+      src = a.F + ((size_t)b * N + m) * 3;
+    }
+    L.F[m * 3 + 0] = src[0];
+    L.F[m * 3 + 1] = src[1];
+    L.F[m * 3 + 2] = src[2];
+    L.slot[m] = s;
+    L.front_of[m] = -1;
+    L.sel[m] = 0;
+  }
+  for (int r = tid; r < R * 3; r += SURV_T) L.ref[r] = a.ref[r];
+  for (int q = tid; q < NW; q += SURV_T) {
+    L.ranked[q] = 0ull;
+    L.cur[q] = 0ull;
+  }
+  __syncthreads();
+
+  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population
+  {
+    double mn[3], mx[3], wp[3];
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = __builtin_inf();
+      mx[k] = -__builtin_inf();
+      wp[k] = -__builtin_inf();
+    }
+    for (int m = tid; m < N; m += SURV_T)
+      for (int k = 0; k < 3; ++k) {
+        const double v = L.F[m * 3 + k];
+        mn[k] = min_prop(mn[k], v);
+        mx[k] = max_prop(mx[k], v);
+        wp[k] = max_prop(wp[k], v);
+      }
+    for (int r = tid; r < R; r += SURV_T)
+      for (int k = 0; k < 3; ++k) {
+        const double v = L.ref[r * 3 + k];
+        mn[k] = min_prop(mn[k], v);
+        mx[k] = max_prop(mx[k], v);
+      }
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = wred_min(mn[k]);
+      mx[k] = wred_max(mx[k]);
+      wp[k] = wred_max(wp[k]);
+    }
+    if (lane == 0)
+      for (int k = 0; k < 3; ++k) {
+        L.red[wave * 16 + k] = mn[k];
+        L.red[wave * 16 + 3 + k] = mx[k];
+        L.red[wave * 16 + 6 + k] = wp[k];
+      }
+    __syncthreads();
+    if (tid < 3) {
+      const int k = tid;
+      double vmn = a.ideal[(size_t)b * 3 + k], vmx = a.worst[(size_t)b * 3 + k];
+      double vwp = -__builtin_inf();
+      for (int w = 0; w < SURV_T / 64; ++w) {
+        vmn = min_prop(vmn, L.red[w * 16 + k]);
+        vmx = max_prop(vmx, L.red[w * 16 + 3 + k]);
+        vwp = max_prop(vwp, L.red[w * 16 + 6 + k]);
+      }
+      ideal[k] = vmn;
+      worst[k] = vmx;
+      wpop[k] = vwp;
+    }
+  }
+
+  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j
+  for (int j = wave; j < N; j += SURV_T / 64) {
+    const double fj[3] = {L.F[j * 3], L.F[j * 3 + 1], L.F[j * 3 + 2]};
+    for (int q = 0; q < NW; ++q) {
+      const int i = q * 64 + lane;
+      const bool d = i < N && dominates(&L.F[i * 3], fj);
+      const unsigned long long msk = __ballot(d);
+      if (lane == 0) L.dom[(size_t)j * NW + q] = msk;
+    }
+  }
+  __syncthreads();
+
+  // ---- fast non-dominated sort (discovery order), stop once >= n_survive ranked
+  int* wsum = L.iscal;  // [0..3]
+  int n0 = block_compact(
+      N,
+      [&](int j) {
+        for (int q = 0; q < NW; ++q)
+          if (L.dom[(size_t)j * NW + q]) return false;
+        return true;
+      },
+      L.I, 0, wsum);
+  for (int k = tid; k < n0; k += SURV_T) {
+    const int j = L.I[k];
+    L.pos[j] = k;
+    L.front_of[j] = 0;
+    atomicOr(&L.ranked[j >> 6], 1ull << (j & 63));
+    atomicOr(&L.cur[j >> 6], 1ull << (j & 63));
+  }
+  if (tid == 0) {
+    L.fstart[0] = 0;
+    L.fstart[1] = n0;
+  }
+  __syncthreads();
+  int cum = n0, nf = 1;
+  while (cum < a.n_survive && cum < N) {
+    const int nc = block_compact(
+        N,
+        [&](int j) {
+          if ((L.ranked[j >> 6] >> (j & 63)) & 1ull) return false;
+          for (int q = 0; q < NW; ++q)
+            if (L.dom[(size_t)j * NW + q] & ~L.ranked[q]) return false;
+          return true;
+        },
+        L.memb, 0, wsum);
+    if (nc == 0) break;  // unreachable for an acyclic dominance relation
+    for (int k = tid; k < nc; k += SURV_T) {
+      const int j = L.memb[k];
+      int mx = -1;
+      for (int q = 0; q < NW; ++q) {
+        unsigned long long bits = L.dom[(size_t)j * NW + q] & L.cur[q];
+        while (bits) {
+          const int i = q * 64 + __ffsll((long long)bits) - 1;
+          bits &= bits - 1ull;
+          mx = L.pos[i] > mx ? L.pos[i] : mx;
+        }
+      }
+      L.key[k] = mx * N + j;
+    }
+    __syncthreads();
+    for (int k = tid; k < nc; k += SURV_T) {
+      const int kk = L.key[k];
+      int r = 0;
+      for (int t = 0; t < nc; ++t) r += L.key[t] < kk;
+      L.I[cum + r] = L.memb[k];
+    }
+    for (int q = tid; q < NW; q += SURV_T) L.cur[q] = 0ull;
+    __syncthreads();
+    for (int k = tid; k < nc; k += SURV_T) {
+      const int j = L.I[cum + k];
+      L.pos[j] = k;
+      L.front_of[j] = nf;
+      atomicOr(&L.ranked[j >> 6], 1ull << (j & 63));
+      atomicOr(&L.cur[j >> 6], 1ull << (j & 63));
+    }
+    cum += nc;
+    ++nf;
+    if (tid == 0) L.fstart[nf] = cum;
+    __syncthreads();
+  }
+  const int n_ranked = cum;
+
+  // ---- extreme points (ASF over prev extremes + front 0 + ref points), worst of front
+  {
+    const int has = a.has_extreme[b] != 0;
+    const int ne = has ? 3 : 0;
+    const int ncand = ne + n0 + R;
+    double bv[3];
+    int bi[3];
+    double wf[3];
+    for (int k = 0; k < 3; ++k) {
+      bv[k] = __builtin_inf();
+      bi[k] = INT_MAX;
+      wf[k] = -__builtin_inf();
+    }
+    for (int c = tid; c < ncand; c += SURV_T) {
+      double row[3];
+      if (c < ne) {
+        for (int k = 0; k < 3; ++k) row[k] = a.extreme[(size_t)b * 9 + c * 3 + k];
+      } else if (c < ne + n0) {
+        const int m = L.I[c - ne];
+        for (int k = 0; k < 3; ++k) {
+          row[k] = L.F[m * 3 + k];
+          wf[k] = max_prop(wf[k], row[k]);
+        }
+      } else {
+        for (int k = 0; k < 3; ++k) row[k] = L.ref[(c - ne - n0) * 3 + k];
+      }
+      double d[3];
+      for (int k = 0; k < 3; ++k) {
+        d[k] = row[k] - ideal[k];
+        if (d[k] < 1e-3) d[k] = 0.0;
+      }
+      for (int i = 0; i < 3; ++i) {
+        double asf = -__builtin_inf();
+        for (int k = 0; k < 3; ++k) asf = max_prop(asf, d[k] * (i == k ? 1.0 : 1e6));
+        if (arg_better(asf, c, bv[i], bi[i])) {
+          bv[i] = asf;
+          bi[i] = c;
+        }
+      }
+    }
+    for (int i = 0; i < 3; ++i) {
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv[i], o, 64);
+        const int oi = __shfl_xor(bi[i], o, 64);
+        if (arg_better(ov, oi, bv[i], bi[i])) {
+          bv[i] = ov;
+          bi[i] = oi;
+        }
+      }
+      wf[i] = wred_max(wf[i]);
+    }
+    __syncthreads();
+    if (lane == 0)
+      for (int i = 0; i < 3; ++i) {
+        L.red[wave * 16 + i] = bv[i];
+        L.red[wave * 16 + 3 + i] = (double)bi[i];
+        L.red[wave * 16 + 6 + i] = wf[i];
+      }
+    __syncthreads();
+    if (tid == 0) {
+      for (int i = 0; i < 3; ++i) {
+        double v = L.red[i];
+        int ix = (int)L.red[3 + i];
+        double w = L.red[6 + i];
+        for (int ww = 1; ww < SURV_T / 64; ++ww) {
+          const double ov = L.red[ww * 16 + i];
+          const int oi = (int)L.red[ww * 16 + 3 + i];
+          if (arg_better(ov, oi, v, ix)) {
+            v = ov;
+            ix = oi;
+          }
+          w = max_prop(w, L.red[ww * 16 + 6 + i]);
+        }
+        wfront[i] = w;
+        double row[3];
+        if (ix < ne) {
+          for (int k = 0; k < 3; ++k) row[k] = a.extreme[(size_t)b * 9 + ix * 3 + k];
+        } else if (ix < ne + n0) {
+          const int m = L.I[ix - ne];
+          for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
+        } else {
+          for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
+        }
+        for (int k = 0; k < 3; ++k) ext[i * 3 + k] = row[k];
+      }
+      // nadir (get_nadir_point with the call-site argument swap)
+      double M[3][3], plane[3] = {1.0, 1.0, 1.0};
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) M[i][k] = ext[i * 3 + k] - ideal[k];
+      double Mc[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
+      bool ok = lu_solve3(Mc, plane);
+      double nd[3];
+      if (ok) {
+        double icp[3];
+        for (int k = 0; k < 3; ++k) {
+          icp[k] = 1.0 / plane[k];
+          nd[k] = ideal[k] + icp[k];
+        }
+        bool close = true, small = false;
+        for (int i = 0; i < 3; ++i) {
+          const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
+          close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
+          small = small || (icp[i] <= 1e-6);
+        }
+        if (!close || small) {
+          ok = false;
+        } else {
+          for (int k = 0; k < 3; ++k)
+            if (nd[k] > worst[k]) nd[k] = worst[k];
+        }
+      }
+      if (!ok)
+        for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
+      for (int k = 0; k < 3; ++k) {
+        if (nd[k] - ideal[k] <= 1e-6) nd[k] = wfront[k];
+        nadir[k] = nd[k];
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- aspiration reference directions (normalised), R points + 3 extreme axes
+  {
+    const double nv = 1.0 / sqrt(3.0);
+    const double asp = a.mu * (1.0 / 3.0);
+    for (int r = tid; r < RN; r += SURV_T) {
+      double res[3];
+      if (r < R) {
+        double l[3];
+        for (int k = 0; k < 3; ++k) l[k] = (L.ref[r * 3 + k] - ideal[k]) / (nadir[k] - ideal[k]);
+        const double dot = (l[0] * nv + l[1] * nv) + l[2] * nv;
+        double inter[3];
+        if (fabs(dot) > 1e-6) {
+          const double d = ((1.0 * nv + 0.0 * nv) + 0.0 * nv) / dot;
+          for (int k = 0; k < 3; ++k) inter[k] = 0.0 + l[k] * d;
+        } else {
+          const double q0 = l[0] - 1.0, q1 = l[1] - 0.0, q2 = l[2] - 0.0;
+          const double t = (q0 * nv + q1 * nv) + q2 * nv;
+          for (int k = 0; k < 3; ++k) inter[k] = l[k] - t * nv;
+        }
+        for (int k = 0; k < 3; ++k) res[k] = asp + (inter[k] - asp);
+        if (!(res[0] > 0.0 && res[1] > 0.0 && res[2] > 0.0)) {
+          for (int k = 0; k < 3; ++k)
+            if (res[k] < 0.0) res[k] = 0.0;
+          const double s = (res[0] + res[1]) + res[2];
+          for (int k = 0; k < 3; ++k) res[k] = res[k] / s;
+        }
+      } else {
+        for (int k = 0; k < 3; ++k) res[k] = (k == r - R) ? 1.0 : 0.0;
+      }
+      const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
+      for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
+    }
+    __syncthreads();
+  }
+
+  // ---- association of the ranked individuals (I order) to the nearest direction
+  {
+    double den[3];
+    for (int k = 0; k < 3; ++k) {
+      den[k] = nadir[k] - ideal[k];
+      if (den[k] == 0.0) den[k] = 1e-12;
+    }
+    for (int p = tid; p < n_ranked; p += SURV_T) {
+      const int m = L.I[p];
+      double Nn[3];
+      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      double best = __builtin_inf();
+      int bj = 0;
+      bool flag = false;
+      for (int j = 0; j < RN; ++j) {
+        const double* u = &L.U[j * 3];
+        const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+        const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+        const double d2 = (e0 * e0 + e1 * e1) + e2 * e2;
+        if (d2 != d2) {
+          flag = true;
+        } else if (d2 < best) {
+          if (best <= d2 * (1.0 + 1e-15)) flag = true;
+          best = d2;
+          bj = j;
+        } else if (d2 <= best * (1.0 + 1e-15)) {
+          flag = true;
+        }
+      }
+      double bd = sqrt(best);
+      if (flag) {  // exact np.argmin over sqrt'ed distances
+        bd = __builtin_inf();
+        bj = 0;
+        for (int j = 0; j < RN; ++j) {
+          const double* u = &L.U[j * 3];
+          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+          if (arg_better(dd, j, bd, bj)) {
+            bd = dd;
+            bj = j;
+          }
+        }
+      }
+      L.niche[p] = bj;
+      L.dist[p] = bd;
+    }
+    __syncthreads();
+  }
+
+  // ---- survivor selection: fronts until the last + niching on the last front
+  int n_out;
+  if (n_ranked > a.n_survive) {
+    const int fs = L.fstart[nf - 1];
+    const int Lc = n_ranked - fs;
+    const int n_rem = nf == 1 ? a.n_survive : a.n_survive - fs;
+    const int until = nf == 1 ? 0 : fs;
+    for (int n = tid; n < RN; n += SURV_T) {
+      L.count[n] = 0;
+      L.remain[n] = 0;
+    }
+    __syncthreads();
+    for (int p = tid; p < until; p += SURV_T) atomicAdd(&L.count[L.niche[p]], 1);
+    for (int p = tid; p < Lc; p += SURV_T) atomicAdd(&L.remain[L.niche[fs + p]], 1);
+    for (int p = tid; p < Lc; p += SURV_T) L.sel[p] = 1;  // mask over last-front positions
+    __syncthreads();
+    if (tid == 0) {  // CSR offsets (RN small)
+      int acc = 0;
+      for (int n = 0; n < RN; ++n) {
+        L.csr_off[n] = acc;
+        acc += L.remain[n];
+      }
+      L.csr_off[RN] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {  // fill in ascending position order (deterministic)
+      for (int n = 0; n < RN; ++n) L.cand[n] = L.csr_off[n];
+      for (int p = 0; p < Lc; ++p) L.csr[L.cand[L.niche[fs + p]]++] = p;
+    }
+    __syncthreads();
+    const Rng rng(a.seed, a.stream_key);
+    int nsel = 0, round = 0;
+    while (nsel < n_rem) {
+      const int n_select = n_rem - nsel;
+      int mn = INT_MAX;
+      for (int n = tid; n < RN; n += SURV_T)
+        if (L.remain[n] > 0 && L.count[n] < mn) mn = L.count[n];
+      mn = wred_imin(mn);
+      if (lane == 0) wsum[wave] = mn;
+      __syncthreads();
+      int gmin = INT_MAX;
+      for (int w = 0; w < SURV_T / 64; ++w) gmin = wsum[w] < gmin ? wsum[w] : gmin;
+      __syncthreads();
+      const int nc = block_compact(
+          RN, [&](int n) { return L.remain[n] > 0 && L.count[n] == gmin; }, L.cand, 0, wsum);
+      for (int k = tid; k < nc; k += SURV_T)
+        L.ckey[k] = (int)rng.draw((uint32_t)(round * RN + L.cand[k]), (uint32_t)a.gen,
+                                  TAG_NICHE_PERM).x;
+      __syncthreads();
+      for (int k = tid; k < nc; k += SURV_T) {
+        const unsigned kk = (unsigned)L.ckey[k];
+        const int nk = L.cand[k];
+        int r = 0;
+        for (int t = 0; t < nc; ++t) {
+          const unsigned kt = (unsigned)L.ckey[t];
+          r += kt < kk || (kt == kk && L.cand[t] < nk);
+        }
+        if (r < n_select) {
+          const bool zero = L.count[nk] == 0;
+          int best = -1;
+          unsigned bkey = 0u;
+          double bdist = 0.0;
+          for (int q = L.csr_off[nk]; q < L.csr_off[nk + 1]; ++q) {
+            const int pp = L.csr[q];
+            if (!L.sel[pp]) continue;
+            const unsigned km =
+                rng.draw((uint32_t)(round * Lc + pp), (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
+            const double dd = L.dist[fs + pp];
+            bool take;
+            if (best < 0) {
+              take = true;
+            } else if (zero && dd != bdist) {
+              take = dd < bdist;
+            } else {
+              take = km < bkey || (km == bkey && pp < best);
+            }
+            if (take) {
+              best = pp;
+              bkey = km;
+              bdist = dd;
+            }
+          }
+          L.surv[until + nsel + r] = fs + best;
+          L.sel[best] = 0;
+          L.count[nk] += 1;
+          L.remain[nk] -= 1;
+        }
+      }
+      __syncthreads();
+      nsel += nc < n_select ? nc : n_select;
+      ++round;
+    }
+    for (int p = tid; p < until; p += SURV_T) L.surv[p] = p;
+    n_out = a.n_survive;
+  } else {
+    for (int p = tid; p < n_ranked; p += SURV_T) L.surv[p] = p;
+    n_out = n_ranked;
+  }
+  __syncthreads();
+
+  // ---- outputs
+  for (int k = tid; k < N; k += SURV_T) L.memb[k] = 0;  // selected flags by merged index
+  __syncthreads();
+  for (int k = tid; k < n_out; k += SURV_T) {
+    const int m = L.I[L.surv[k]];
+    L.memb[m] = 1;
+    L.sel[k] = L.slot[m];  // new population order -> slot (read by the tournament below)
+    if (slot_mode)
+      a.pop_slot_out[(size_t)b * a.n_survive + k] = L.slot[m];
+    else
+      a.survivors[(size_t)b * a.n_survive + k] = m;
+  }
+  if (!slot_mode)
+    for (int k = n_out + tid; k < a.n_survive; k += SURV_T)
+      a.survivors[(size_t)b * a.n_survive + k] = -1;
+  if (a.rank)
+    for (int m = tid; m < N; m += SURV_T) a.rank[(size_t)b * N + m] = L.front_of[m];
+  if (a.order)
+    for (int p = tid; p < N; p += SURV_T) a.order[(size_t)b * N + p] = p < n_ranked ? L.I[p] : -1;
+  if (a.niche)
+    for (int p = tid; p < N; p += SURV_T) a.niche[(size_t)b * N + p] = p < n_ranked ? L.niche[p] : -1;
+  if (a.dist)
+    for (int p = tid; p < N; p += SURV_T)
+      a.dist[(size_t)b * N + p] = p < n_ranked ? L.dist[p] : 0.0;
+  if (tid == 0) {
+    if (a.n_ranked) a.n_ranked[b] = n_ranked;
+    for (int k = 0; k < 3; ++k) {
+      a.ideal[(size_t)b * 3 + k] = ideal[k];
+      a.worst[(size_t)b * 3 + k] = worst[k];
+      if (a.nadir) a.nadir[(size_t)b * 3 + k] = nadir[k];
+    }
+    for (int k = 0; k < 9; ++k) a.extreme[(size_t)b * 9 + k] = ext[k];
+    a.has_extreme[b] = 1;
+  }
+  __syncthreads();
+  if (slot_mode && N > a.n_survive) {
+    const int nfree = block_compact(N, [&](int m) { return L.memb[m] == 0; }, L.key, 0, wsum);
+    for (int k = tid; k < nfree; k += SURV_T)
+      a.free_slot[(size_t)b * a.O + k] = L.slot[L.key[k]];
+  }
+  if (a.parents_out) {
+    __syncthreads();
+    tournament(a.n_survive, a.O_next, a.seed, a.stream_key, a.sel_gen, slot_mode ? L.sel : nullptr,
+               a.parents_out + (size_t)b * n_m_next * 2, L.selkey, L.perm);
+  }
+}
+
+__global__ __launch_bounds__(SURV_T) void k_select(int P, int O, uint64_t seed, uint32_t sk,
+                                                   int gen, const int* pop_slot, int* parents) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int n_m = (O + 1) / 2;
+  const int slots = ((n_m * 4 + P - 1) / P) * P;
+  int* key = (int*)smem;
+  int* perm = key + slots;
+  tournament(P, O, seed, sk, gen, pop_slot ? pop_slot + (size_t)b * P : nullptr,
+             parents + (size_t)b * n_m * 2, key, perm);
+}
+
+__global__ void k_init_pool(int B, int P, int O, int V, int S, const double* genes0, double* pool,
+                            int* pop_slot, int* free_slot) {
+  const size_t tot = (size_t)B * P * V;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = t / ((size_t)P * V);
+    const size_t r = t - b * P * V;
+    const size_t s = r / V, g = r - s * V;
+    pool[(b * S + s) * V + g] = genes0[b * V + g];
+  }
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < (size_t)B * S;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(t / S), s = (int)(t - (size_t)b * S);
+    if (s < P)
+      pop_slot[(size_t)b * P + s] = s;
+    else
+      free_slot[(size_t)b * O + (s - P)] = s;
+  }
+}
+
+__global__ void k_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
+                             const double* poolF, double* genes, double* F) {
+  const size_t tot = (size_t)B * P;
+  for (size_t t = blockIdx.x; t < tot; t += gridDim.x) {
+    const size_t b = t / P;
+    const int s = pop_slot[t];
+    if (genes)
+      for (int g = threadIdx.x; g < V; g += blockDim.x) genes[t * V + g] = pool[(b * S + s) * V + g];
+    if (F && threadIdx.x < 3) F[t * 3 + threadIdx.x] = poolF[(b * S + s) * 3 + threadIdx.x];
+  }
+}
+
+size_t surv_lds_bytes(int N, int R, int Pperm) { return surv_layout(N, R, Pperm, nullptr, nullptr); }
+
+hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  const int n_m = a.parents_out ? (a.O_next + 1) / 2 : 0;
+  const int pslots = a.parents_out ? ((n_m * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
+  const size_t lds = surv_lds_bytes(a.N, a.R, pslots);
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)k_survive, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipGetLastError();
+    configured = true;
+  }
+  hipLaunchKernelGGL(k_survive, dim3(B), dim3(SURV_T), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_select(int B, int P, int O, uint64_t seed, uint32_t sk, int gen,
+                         const int* pop_slot, int* parents, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  const int n_m = (O + 1) / 2;
+  const int slots = ((n_m * 4 + P - 1) / P) * P;
+  hipLaunchKernelGGL(k_select, dim3(B), dim3(SURV_T), (size_t)slots * 8, stream, P, O, seed, sk,
+                     gen, pop_slot, parents);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* genes0, double* pool,
+                            int* pop_slot, int* free_slot, hipStream_t stream) {
+  hipLaunchKernelGGL(k_init_pool, dim3(1024), dim3(256), 0, stream, B, P, O, V, S, genes0, pool,
+                     pop_slot, free_slot);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
+                             const double* poolF, double* genes, double* F, hipStream_t stream) {
+  hipLaunchKernelGGL(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, S, pop_slot, pool,
+                     poolF, genes, F);
+  return hipGetLastError();
+}
+
+}  // namespace mv

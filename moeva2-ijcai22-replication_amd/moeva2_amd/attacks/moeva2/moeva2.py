@@ -1,0 +1,138 @@
+"""MoEvA2 attack API (mirror of src/attacks/moeva2/moeva2.py:35-207).
+
+``generate(x, minimize_class)`` keeps the reference signature, argument checks and return
+type (one EfficientResult / HistoryResult per initial state), but instead of one
+pymoo.minimize per state in a joblib pool (moeva2.py:194-205) it binds ALL states to the
+device and runs the whole R-NSGA-III loop on the MI355X (``mv_attack_run``): initial
+population + evaluation, then (n_gen - 1) x {tournament, two-point crossover +
+polynomial mutation + evaluation, survival}, with no host round trip.
+"""
+import secrets
+
+import numpy as np
+
+from ...problem import get_engine
+from .classifier import Classifier, load_model
+from .constraints import Constraints
+from .feature_encoder import get_encoder_from_constraints
+from .ref_dirs import energy_ref_dirs
+from .result_process import EfficientResult, HistoryResult, Individual, Population
+
+N_OBJ = 3
+MU = 0.05  # RNSGA3 default shrink factor (pymoo 0.4.2.2)
+
+
+def history_mode(save_history) -> int:
+    """default_problem.py:137-140 substring tests on the (string) save_history."""
+    if not save_history:
+        return 0
+    s = str(save_history)
+    if "reduced" in s:
+        return 1
+    if "full" in s:
+        return 2
+    return 0
+
+
+def _non_dominated(F):
+    n = F.shape[0]
+    less = (F[:, None, :] < F[None, :, :]).any(-1)
+    more = (F[:, None, :] > F[None, :, :]).any(-1)
+    dominated = (less & ~more).any(0)
+    return ~dominated
+
+
+class Moeva2:
+    def __init__(self, classifier_path: str, constraints: Constraints, ml_scaler=None,
+                 problem_class=None, l2_ball_size=0.1, norm=np.inf, n_gen=625, n_pop=640,
+                 n_offsprings=320, scale_objectives=True, save_history=False, seed=None,
+                 n_jobs=-1, verbose=1, device: int = 0) -> None:
+        self._classifier_path = classifier_path
+        self._constraints = constraints
+        self._ml_scaler = ml_scaler
+        self._problem_class = problem_class
+        self._n_gen = n_gen
+        self._n_pop = n_pop
+        self._n_offsprings = n_offsprings
+        self._scale_objectives = scale_objectives
+        self._save_history = save_history
+        self._seed = seed
+        self._n_jobs = n_jobs  # the device batch replaces the joblib pool
+        self._verbose = verbose
+        self._encoder = get_encoder_from_constraints(self._constraints)
+        self.l2_ball_size = l2_ball_size
+        self.norm = norm
+        self.device = device
+        self._classifier = None
+        self.last_engine = None
+
+    def _check_input_size(self, x: np.ndarray) -> None:
+        if x.shape[1] != self._encoder.mutable_mask.shape[0]:
+            raise ValueError(
+                f"Mutable mask has shape (n_features,): {self._encoder.mutable_mask.shape[0]}, "
+                f"x has shaper (n_sample, n_features): {x.shape}. n_features must be equal.")
+
+    def _get_classifier(self):
+        if self._classifier is None:
+            self._classifier = Classifier(load_model(self._classifier_path))
+        return self._classifier
+
+    def pop_size(self) -> int:
+        """RNSGA3: n_ref_points * n_aspiration_dirs (1) + n_obj."""
+        return self._n_pop + N_OBJ
+
+    def generate(self, x: np.ndarray, minimize_class, return_device=False):
+        if isinstance(minimize_class, (int, np.integer)):
+            minimize_class = np.repeat(minimize_class, x.shape[0])
+        minimize_class = np.asarray(minimize_class)
+        if x.shape[0] != minimize_class.shape[0]:
+            raise ValueError(
+                "minimize_class argument must be an integer or an array of shaper (x.shape[0])")
+        self._check_input_size(x)
+        if len(x.shape) != 2:
+            raise ValueError(f"x ({x.shape}) must have 2 dimensions.")
+        import torch
+
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        B = x.shape[0]
+        eng = get_engine(self._constraints, self._get_classifier(), self._ml_scaler, self.norm,
+                         self._scale_objectives, self.device)
+        bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
+        xl = np.array([b[0] for b in bounds], np.float64)
+        xu = np.array([b[1] for b in bounds], np.float64)
+        eng.set_states(x, xl, xu, minimize_class)
+        P, O = self.pop_size(), self._n_offsprings
+        seed = self._seed if self._seed is not None else secrets.randbits(63)
+        ref = energy_ref_dirs(N_OBJ, self._n_pop, seed=1)
+        hmode = history_mode(self._save_history)
+        eng.attack_run(self._n_gen, P, O, int(seed), ref, MU, hmode)
+        V = eng.prog.V
+        dev = torch.device("cuda", self.device)
+        genes = torch.empty((B, P, V), dtype=torch.float64, device=dev)
+        F = torch.empty((B, P, 3), dtype=torch.float64, device=dev)
+        eng.attack_population(genes, F)
+        hist = None
+        if hmode:
+            w = 3 if hmode == 1 else 3 + eng.prog.C
+            hist = torch.empty((B, P + (self._n_gen - 1) * O, w), dtype=torch.float64, device=dev)
+            eng.attack_history(hist)
+        self.last_engine = eng
+        if return_device:
+            return genes, F, hist
+        genes_h = genes.cpu().numpy()
+        F_h = F.cpu().numpy()
+        hist_h = hist.cpu().numpy() if hist is not None else None
+        return [self._result(b, x[b], genes_h[b], F_h[b], hist_h, P, O) for b in range(B)]
+
+    def _result(self, b, x0, genes, F, hist, P, O):
+        pop = Population(Individual(genes[i], F[i]) for i in range(P))
+        nd = _non_dominated(F)
+        res = {"pop": pop, "initial_state": x0, "n_gen": self._n_gen, "pop_size": P,
+               "n_offsprings": O, "X": genes[nd], "F": F[nd],
+               "pareto": np.empty((0, genes.shape[1]))}
+        if self._save_history:
+            h = [] if hist is None else [hist[b, :P]] + [
+                hist[b, P + (g - 1) * O: P + g * O] for g in range(1, self._n_gen)]
+            res["history"] = h
+            return HistoryResult(res)
+        return EfficientResult(res)
