@@ -184,6 +184,11 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   K((int**)&p.op_arg, pd->op_arg, (size_t)C * 4);
   K((double**)&p.op_k, pd->op_karg, (size_t)C * 2);
   K((int**)&p.idx_pool, pd->idx_pool, pd->n_pool);
+  std::vector<int> sdo;
+  for (int c = 0; c < C; ++c)
+    if (pd->op_code[c] == MV_OP_ABS_SUMDIFF) sdo.push_back(c);
+  p.n_sumdiff = (int)sdo.size();
+  K((int**)&p.sumdiff_ops, sdo.data(), sdo.size());
   p.tol = pd->tol;
   p.norm = pd->norm;
   p.scale_obj = pd->scale_objectives;

@@ -38,6 +38,8 @@ struct DProblem {
   const int* op_arg;      // [C*4]
   const double* op_k;     // [C*2]
   const int* idx_pool;
+  int n_sumdiff;          // ABS_SUMDIFF ops, evaluated wave-parallel
+  const int* sumdiff_ops; // [n_sumdiff] their column indices
   double tol;
   int norm;               // 2 or 0 (inf)
   int scale_obj;

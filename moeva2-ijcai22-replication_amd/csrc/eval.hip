@@ -109,6 +109,18 @@ __device__ double eval_op(const DProblem& p, int c, const double* __restrict__ x
   }
 }
 
+// |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes (exact for the integer-valued
+// features of every shipped program; summation order differs from numpy otherwise).
+__device__ __forceinline__ double sumdiff_wave(const DProblem& p, int c, const double* x, int lane) {
+  const int* ar = p.op_arg + 4 * c;
+  double s0 = 0.0, s1 = 0.0;
+  for (int q = ar[0] + lane; q < ar[1]; q += 64) s0 += x[p.idx_pool[q]];
+  for (int q = ar[1] + lane; q < ar[2]; q += 64) s1 += x[p.idx_pool[q]];
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  return fabs(s0 - s1);
+}
+
 // pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction.
 __device__ __forceinline__ double poly_mut(double x, double xl, double xu, double u, double eta) {
   const double d1 = (x - xl) / (xu - xl);
@@ -379,12 +391,24 @@ __global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
                          ? a.hist + ((size_t)b * a.hist_rows + a.hist_row0 + i) * a.hist_w + 3
                          : nullptr;
       for (int c = lane; c < p.C; c += 64) {
+        if (p.op_code[c] == 3) continue;  // ABS_SUMDIFF: wave-parallel below
         double v = eval_op(p, c, xrow);
         if (v <= p.tol) v = 0.0;
         const double g = v * (v > 0.0 ? 1.0 : 0.0);
         if (grow) grow[c] = g;
         if (hrow) hrow[c] = g;
         acc3 += g;
+      }
+      for (int k = 0; k < p.n_sumdiff; ++k) {
+        const int c = p.sumdiff_ops[k];
+        double v = sumdiff_wave(p, c, xrow, lane);
+        if (v <= p.tol) v = 0.0;
+        const double g = v * (v > 0.0 ? 1.0 : 0.0);
+        if (lane == 0) {
+          if (grow) grow[c] = g;
+          if (hrow) hrow[c] = g;
+          acc3 += g;
+        }
       }
       acc3 = wave_sum(acc3);
       if (lane == 0) {
@@ -532,9 +556,16 @@ __global__ __launch_bounds__(256) void k_constraints(DProblem p, int n, const do
   __syncthreads();
   if (r >= n) return;
   for (int c = lane; c < p.C; c += 64) {
+    if (p.op_code[c] == 3) continue;
     double v = eval_op(p, c, xrow);
     if (v <= p.tol) v = 0.0;
     G[(size_t)r * p.C + c] = v;
+  }
+  for (int k = 0; k < p.n_sumdiff; ++k) {
+    const int c = p.sumdiff_ops[k];
+    double v = sumdiff_wave(p, c, xrow, lane);
+    if (v <= p.tol) v = 0.0;
+    if (lane == 0) G[(size_t)r * p.C + c] = v;
   }
 }
 

@@ -52,6 +52,9 @@ struct SurvLds {
   int* iscal;       // [16]
   int* selkey;      // [n_perm_slots]
   int* perm;        // [n_perm_slots]
+  unsigned long long* dmin;  // [R+3]
+  int* lhist;       // [2N+2] picks per level -> prefix
+  int* lround;      // [2N+2] round index of each level
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -73,7 +76,9 @@ __host__ __device__ inline size_t surv_layout(int N, int R, int Pperm, SurvLds* 
                oSurv = take(N * 4), oSel = take(N * 4), oFs = take((N + 2) * 4),
                oCnt = take(RN * 4), oRem = take(RN * 4), oCo = take((RN + 1) * 4),
                oCsr = take(N * 4), oCand = take(RN * 4), oCk = take(RN * 4), oIs = take(16 * 4),
-               oSk = take((size_t)Pperm * 4), oPerm = take((size_t)Pperm * 4);
+               oSk = take((size_t)Pperm * 4), oPerm = take((size_t)Pperm * 4),
+               oDmin = take((size_t)RN * 8), oLh = take((size_t)(2 * N + 2) * 4),
+               oLr = take((size_t)(2 * N + 2) * 4);
   if (L) {
     L->F = (double*)(base + oF);
     L->ref = (double*)(base + oRef);
@@ -103,6 +108,9 @@ __host__ __device__ inline size_t surv_layout(int N, int R, int Pperm, SurvLds* 
     L->iscal = (int*)(base + oIs);
     L->selkey = (int*)(base + oSk);
     L->perm = (int*)(base + oPerm);
+    L->dmin = (unsigned long long*)(base + oDmin);
+    L->lhist = (int*)(base + oLh);
+    L->lround = (int*)(base + oLr);
   }
   return off;
 }
@@ -164,14 +172,6 @@ __device__ __forceinline__ double wred_max(double v) {
   for (int o = 32; o > 0; o >>= 1) v = max_prop(v, __shfl_xor(v, o, 64));
   return v;
 }
-__device__ __forceinline__ int wred_imin(int v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const int w = __shfl_xor(v, o, 64);
-    v = w < v ? w : v;
-  }
-  return v;
-}
-
 // LAPACK dgetf2/dgetrs-order 3x3 solve (oracle lu_solve3).  Returns false if singular.
 __device__ bool lu_solve3(double A[3][3], double x[3]) {
   for (int k = 0; k < 3; ++k) {
@@ -618,94 +618,113 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   // ---- survivor selection: fronts until the last + niching on the last front
   int n_out;
   if (n_ranked > a.n_survive) {
+    // Niching in closed form.  With member keys fixed per generation, niche n's picks
+    // follow one order (min-dist member first when its until-front count c_n is 0, then
+    // ascending (key, position)); its j-th pick happens at "level" c_n + j, the loop's
+    // rounds visit the non-empty levels in ascending order, and within a round the
+    // niches go in ascending (round key, niche).  So every pick's output position is a
+    // prefix count over levels plus a rank inside its level: no sequential loop.
     const int fs = L.fstart[nf - 1];
     const int Lc = n_ranked - fs;
     const int n_rem = nf == 1 ? a.n_survive : a.n_survive - fs;
     const int until = nf == 1 ? 0 : fs;
+    const Rng rng(a.seed, a.stream_key);
+    int* mkey = L.key;
+    int* grank = L.memb;
+    int* lev = L.csr;
+    int* K = L.pos;
+    int* cnt = L.count;
+    int* mcnt = L.remain;
+    int* start = L.csr_off;
+    int* bestkr = L.cand;
+    const int* nich = L.niche + fs;
+    const double* dst = L.dist + fs;
+    const int nlev = N + Lc + 1;
     for (int n = tid; n < RN; n += SURV_T) {
-      L.count[n] = 0;
-      L.remain[n] = 0;
+      cnt[n] = 0;
+      mcnt[n] = 0;
+      L.dmin[n] = ~0ull;
+      bestkr[n] = INT_MAX;
+    }
+    for (int l = tid; l <= nlev; l += SURV_T) L.lhist[l] = 0;
+    __syncthreads();
+    for (int p = tid; p < until; p += SURV_T) atomicAdd(&cnt[L.niche[p]], 1);
+    for (int p = tid; p < Lc; p += SURV_T) {
+      atomicAdd(&mcnt[nich[p]], 1);
+      mkey[p] = (int)rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
     }
     __syncthreads();
-    for (int p = tid; p < until; p += SURV_T) atomicAdd(&L.count[L.niche[p]], 1);
-    for (int p = tid; p < Lc; p += SURV_T) atomicAdd(&L.remain[L.niche[fs + p]], 1);
-    for (int p = tid; p < Lc; p += SURV_T) L.sel[p] = 1;  // mask over last-front positions
-    __syncthreads();
-    if (tid == 0) {  // CSR offsets (RN small)
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int np_ = nich[p];
+      const unsigned kp = (unsigned)mkey[p];
+      int r = 0;
+      for (int q = 0; q < Lc; ++q) {
+        const int nq = nich[q];
+        const unsigned kq = (unsigned)mkey[q];
+        r += (nq < np_) || (nq == np_ && (kq < kp || (kq == kp && q < p)));
+      }
+      grank[p] = r;
+      if (cnt[np_] == 0)
+        atomicMin(&L.dmin[np_], (unsigned long long)__double_as_longlong(dst[p]));
+    }
+    if (tid == 0) {
       int acc = 0;
       for (int n = 0; n < RN; ++n) {
-        L.csr_off[n] = acc;
-        acc += L.remain[n];
+        start[n] = acc;
+        acc += mcnt[n];
       }
-      L.csr_off[RN] = acc;
     }
     __syncthreads();
-    if (tid == 0) {  // fill in ascending position order (deterministic)
-      for (int n = 0; n < RN; ++n) L.cand[n] = L.csr_off[n];
-      for (int p = 0; p < Lc; ++p) L.csr[L.cand[L.niche[fs + p]]++] = p;
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int np_ = nich[p];
+      if (cnt[np_] == 0 && (unsigned long long)__double_as_longlong(dst[p]) == L.dmin[np_])
+        atomicMin(&bestkr[np_], grank[p] - start[np_]);
     }
     __syncthreads();
-    const Rng rng(a.seed, a.stream_key);
-    int nsel = 0, round = 0;
-    while (nsel < n_rem) {
-      const int n_select = n_rem - nsel;
-      int mn = INT_MAX;
-      for (int n = tid; n < RN; n += SURV_T)
-        if (L.remain[n] > 0 && L.count[n] < mn) mn = L.count[n];
-      mn = wred_imin(mn);
-      if (lane == 0) wsum[wave] = mn;
-      __syncthreads();
-      int gmin = INT_MAX;
-      for (int w = 0; w < SURV_T / 64; ++w) gmin = wsum[w] < gmin ? wsum[w] : gmin;
-      __syncthreads();
-      const int nc = block_compact(
-          RN, [&](int n) { return L.remain[n] > 0 && L.count[n] == gmin; }, L.cand, 0, wsum);
-      for (int k = tid; k < nc; k += SURV_T)
-        L.ckey[k] = (int)rng.draw((uint32_t)(round * RN + L.cand[k]), (uint32_t)a.gen,
-                                  TAG_NICHE_PERM).x;
-      __syncthreads();
-      for (int k = tid; k < nc; k += SURV_T) {
-        const unsigned kk = (unsigned)L.ckey[k];
-        const int nk = L.cand[k];
-        int r = 0;
-        for (int t = 0; t < nc; ++t) {
-          const unsigned kt = (unsigned)L.ckey[t];
-          r += kt < kk || (kt == kk && L.cand[t] < nk);
-        }
-        if (r < n_select) {
-          const bool zero = L.count[nk] == 0;
-          int best = -1;
-          unsigned bkey = 0u;
-          double bdist = 0.0;
-          for (int q = L.csr_off[nk]; q < L.csr_off[nk + 1]; ++q) {
-            const int pp = L.csr[q];
-            if (!L.sel[pp]) continue;
-            const unsigned km =
-                rng.draw((uint32_t)(round * Lc + pp), (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
-            const double dd = L.dist[fs + pp];
-            bool take;
-            if (best < 0) {
-              take = true;
-            } else if (zero && dd != bdist) {
-              take = dd < bdist;
-            } else {
-              take = km < bkey || (km == bkey && pp < best);
-            }
-            if (take) {
-              best = pp;
-              bkey = km;
-              bdist = dd;
-            }
-          }
-          L.surv[until + nsel + r] = fs + best;
-          L.sel[best] = 0;
-          L.count[nk] += 1;
-          L.remain[nk] -= 1;
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int np_ = nich[p];
+      const int kr = grank[p] - start[np_];
+      int j = kr;
+      if (cnt[np_] == 0) j = kr == bestkr[np_] ? 0 : kr + (kr < bestkr[np_] ? 1 : 0);
+      const int l = cnt[np_] + j;
+      lev[p] = l;
+      atomicAdd(&L.lhist[l], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0, rnd = 0;
+      for (int l = 0; l < nlev; ++l) {
+        const int h = L.lhist[l];
+        L.lhist[l] = acc;
+        L.lround[l] = rnd;
+        if (h) {
+          acc += h;
+          ++rnd;
         }
       }
-      __syncthreads();
-      nsel += nc < n_select ? nc : n_select;
-      ++round;
+      L.lhist[nlev] = acc;
+    }
+    __syncthreads();
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int l = lev[p];
+      if (L.lhist[l] < n_rem)
+        K[p] = (int)rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
+                             TAG_NICHE_PERM).x;
+    }
+    __syncthreads();
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int l = lev[p];
+      const int base = L.lhist[l];
+      if (base >= n_rem) continue;
+      const unsigned kp = (unsigned)K[p];
+      const int np_ = nich[p];
+      int r = 0;
+      for (int q = 0; q < Lc; ++q) {
+        if (lev[q] != l) continue;
+        const unsigned kq = (unsigned)K[q];
+        r += kq < kp || (kq == kp && nich[q] < np_);
+      }
+      if (base + r < n_rem) L.surv[until + base + r] = fs + p;
     }
     for (int p = tid; p < until; p += SURV_T) L.surv[p] = p;
     n_out = a.n_survive;

@@ -601,10 +601,13 @@ def associate(F, ref_dirs, ideal, nadir):
 
 def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
     """[pymoo-recall] nsga3.niching with Philox draws replacing np.random:
-    * ``np.random.permutation(next_niches)[:n_select]`` -> niches ordered by
-      (key(TAG_NICHE_PERM, round*n_niches + niche), niche);
-    * ``np.random.shuffle(members)`` then argmin/first -> member with the smallest
-      (key(TAG_NICHE_MEMBER, round*L + position), position) among the eligible ones."""
+    * ``np.random.permutation(next_niches)[:n_select]`` in loop iteration ``round`` ->
+      niches ordered by (key(TAG_NICHE_PERM, round*n_niches + niche), niche);
+    * ``np.random.shuffle(members)`` then argmin/first -> among the eligible members the
+      smallest (key(TAG_NICHE_MEMBER, position), position), the member keys being drawn once
+      per generation.  Successive uniform picks without replacement (the reference's fresh
+      shuffle per round) and picks in the order of one random permutation have the same
+      distribution; fixing the keys makes each niche's pick order a single sort."""
     niche_count = np.array(niche_count, dtype=np.int64, copy=True)
     L = len(niche_of)
     n_niches = len(niche_count)
@@ -613,6 +616,7 @@ def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
     rnd = 0
     sp = px.Stream(seed, gen, px.TAG_NICHE_PERM, stream_key)
     sm = px.Stream(seed, gen, px.TAG_NICHE_MEMBER, stream_key)
+    km = sm.words(np.arange(L))[0].astype(np.int64)
     while len(survivors) < n_remaining:
         n_select = n_remaining - len(survivors)
         nl = np.unique(niche_of[mask])
@@ -621,7 +625,6 @@ def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
         kn = sp.words(rnd * n_niches + cand)[0].astype(np.int64)
         order = np.lexsort((cand, kn))
         cand = cand[order][:n_select]
-        km = sm.words(rnd * L + np.arange(L))[0].astype(np.int64)
         for nn in cand:
             members = np.where((niche_of == nn) & mask)[0]
             if niche_count[nn] == 0:

@@ -13,6 +13,9 @@ for s in $STEPS; do
              > gpurun_out/smoke.log 2>&1; rc=$? ;;
     bench) timeout -k 10 600 python -u bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --cpu-gens 30} \
              > gpurun_out/bench.json 2> gpurun_out/bench.log; rc=$? ;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
+             --output-format csv -- python3 bench.py ${PROF_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --n-gen 200} \
+             > gpurun_out/prof.log 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=1 ;;
   esac
   echo "step $s rc=$rc"
@@ -21,3 +24,4 @@ done
 tail -5 gpurun_out/gpu_tests.log 2>/dev/null
 cat gpurun_out/smoke.log 2>/dev/null | tail -3
 cat gpurun_out/bench.json 2>/dev/null
+find gpurun_out/prof -name '*kernel_stats.csv' 2>/dev/null | head -1 | xargs -r head -12
