@@ -42,6 +42,11 @@ WORKLOADS = {
 }
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector peak)
+
+
+def eng_dims(eng):
+    return eng.dims
 
 
 def log(*a):
@@ -171,18 +176,27 @@ def main():
     value = total_evals / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # ---- roofline of the dominant kernel (fused variation + evaluation), measured live with
-    # HIP events recorded by the engine around each launch on the bench stream
+    # ---- roofline of the dominant kernels, measured live with HIP events that the engine
+    # records on the bench stream around every k_vary / k_mlp / k_survive launch
     eng.set_profiling(True)
     eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
     eng.set_profiling(False)
-    var_ms = kt["vareval_ms"] / max(kt["n_vareval"], 1)
-    surv_ms = kt["survive_ms"] / max(kt["n_survive"], 1)
-    bytes_per_eval = 2 * V * 8 + 24  # write+read offspring genes + F
+    ng = max(kt["generations"], 1)
+    vary_ms = kt["vary_ms"] / ng
+    mlp_ms = kt["mlp_ms"] / ng
+    surv_ms = kt["survive_ms"] / ng
     rows = B * O
-    achieved = bytes_per_eval * rows / (var_ms * 1e-3) / 1e9
+    Dm4 = (int(eng.prog.mut_feats.shape[0]) + 3) // 4 * 4
+    # k_vary algorithmic bytes per offspring row (SURVEY.md §8d form): parent genes read +
+    # child genes written (2*V*8) + f2/f3 (16) + the fp32 ML row handed to k_mlp (Dm4*4)
+    vary_bytes = 2 * V * 8 + 16 + Dm4 * 4
+    vary_gbs = vary_bytes * rows / (vary_ms * 1e-3) / 1e9
+    dims = [int(eng.prog.mut_feats.shape[0])] + list(eng_dims(eng))[1:]
+    mlp_flops = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+    mlp_tfs = mlp_flops * rows / (mlp_ms * 1e-3) / 1e12
+    dom = max(("k_vary", vary_ms), ("k_mlp", mlp_ms), ("k_survive", surv_ms), key=lambda t: t[1])
 
     result = {
         "metric": "candidate fitness evals/sec (whole node) + attack wall-clock per 1k states",
@@ -205,13 +219,17 @@ def main():
                    "parallelism": f"states x{world} (independent per-rank shards)"},
         "attack_wall_clock_per_1k_states_s": elapsed / args.steps / (world * B) * 1000.0,
         "load_s": load_s,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_rows<1> (fused variation + evaluation)",
-                     "algorithmic_bytes_per_launch": bytes_per_eval * rows,
-                     "avg_launch_ms": var_ms},
-        "kernels_avg_ms": {"vareval": var_ms, "survive": surv_ms,
-                           "launches": kt["n_vareval"] + kt["n_survive"]},
+        "roofline": {"bound": "hbm", "achieved": vary_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": vary_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_vary (variation + decode + constraints + distance)",
+                     "algorithmic_bytes_per_launch": vary_bytes * rows,
+                     "avg_launch_ms": vary_ms},
+        "mlp_roofline": {"bound": "mfma", "achieved": mlp_tfs, "peak": MFMA_F32_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": mlp_tfs / MFMA_F32_PEAK_TFS,
+                         "kernel": "k_mlp (fp32 MFMA Dense chain)",
+                         "algorithmic_flops_per_launch": mlp_flops * rows, "avg_launch_ms": mlp_ms},
+        "kernels_avg_ms_per_generation": {"k_vary": vary_ms, "k_mlp": mlp_ms, "k_survive": surv_ms,
+                                          "dominant": dom[0]},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline(w, 1, args.cpu_gens)

@@ -158,10 +158,11 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
 /* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
 int mv_attack_history(mv_engine* e, double* hist, void* stream);
-/* Per-kernel timing of the last mv_attack_run when enabled (HIP events on `stream`). */
+/* Per-kernel timing of the last mv_attack_run when enabled: HIP events recorded on the
+ * run's stream around k_vary, k_mlp and k_survive of every generation (summed ms). */
 int mv_set_profiling(mv_engine* e, int32_t enabled);
-int mv_get_kernel_times(mv_engine* e, double* vareval_ms, double* survive_ms,
-                        int32_t* n_vareval, int32_t* n_survive);
+int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
+                        int32_t* n_generations);
 
 #ifdef __cplusplus
 }

@@ -84,9 +84,21 @@ struct mv_engine {
   double* hist = nullptr;
   bool attack_ready = false;
   bool has_model = false;
+  float* xml = nullptr;  // k_vary -> k_mlp scratch
+  size_t xml_cap = 0;
+  hipError_t ensure_xml(size_t rows) {
+    const size_t need = rows * (size_t)p.Dm4;
+    if (need <= xml_cap) return hipSuccess;
+    if (xml) (void)hipFree(xml);
+    xml = nullptr;
+    xml_cap = 0;
+    hipError_t e = hipMalloc((void**)&xml, need * sizeof(float));
+    if (e == hipSuccess) xml_cap = need;
+    return e;
+  }
   // profiling
   bool profiling = false;
-  std::vector<hipEvent_t> ev_var, ev_surv;
+  std::vector<hipEvent_t> ev_var, ev_mlp, ev_surv;
   int n_var_rec = 0, n_surv_rec = 0;
 
   void free_list(std::vector<void*>& v) {
@@ -101,10 +113,12 @@ struct mv_engine {
   }
   ~mv_engine() {
     (void)hipSetDevice(device);
+    if (xml) (void)hipFree(xml);
     free_list(attack_allocs);
     free_list(state_allocs);
     free_list(prob_allocs);
     for (auto e : ev_var) (void)hipEventDestroy(e);
+    for (auto e : ev_mlp) (void)hipEventDestroy(e);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
   }
 };
@@ -175,11 +189,31 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   K((int**)&p.gene_kind, pd->gene_kind, V);
   K((int**)&p.gene_feat, pd->gene_feat, V);
   K((int**)&p.gene_sub, sub.data(), V);
+  const int V4 = (V + 3) & ~3;
+  std::vector<int> info(V4, 0);
+  for (int g = 0; g < V; ++g) {
+    if (pd->gene_feat[g] < 0 || pd->gene_feat[g] > 0x7FFF || sub[g] > 0x7FFF) {
+      delete e;
+      return fail(MV_ERR_ARG, "feature/gene index too large for the packed gene table");
+    }
+    info[g] = pd->gene_kind[g] | (sub[g] << 2) | (pd->gene_feat[g] << 17);
+  }
+  K((int**)&p.gene_info, info.data(), V4);
   K((int**)&p.ohe_off, ohe_off.data(), ohe_off.size());
   K((int**)&p.ohe_feat, pd->ohe_feats, n_ohe_feats);
   K((int**)&p.mut_feat, pd->mut_feats, Dm);
   K((double**)&p.ml_scale, mls.data(), D);
   K((double**)&p.ml_min, mlm.data(), D);
+  {
+    const int Dm4 = (Dm + 3) & ~3;
+    std::vector<double> ms(Dm4, 0.0), mm(Dm4, 0.0);
+    for (int j = 0; j < Dm; ++j) {
+      ms[j] = mls[pd->mut_feats[j]];
+      mm[j] = mlm[pd->mut_feats[j]];
+    }
+    K((double**)&p.mlS, ms.data(), Dm4);
+    K((double**)&p.mlM, mm.data(), Dm4);
+  }
   K((int**)&p.op_code, pd->op_code, C);
   K((int**)&p.op_arg, pd->op_arg, (size_t)C * 4);
   K((double**)&p.op_k, pd->op_karg, (size_t)C * 2);
@@ -224,8 +258,8 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   }
   int hmax = 16;
   for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
-  const size_t lds = eval_lds_bytes(D, p.Dm4, hmax);
-  if (md && lds > 160 * 1024) {
+  const size_t lds = mlp_lds_bytes(p.Dm4, hmax);
+  if (md && (lds > 160 * 1024 || (size_t)4 * D * 8 > 160 * 1024)) {
     delete e;
     return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
   }
@@ -300,6 +334,8 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
   a.out_rows = n;
   a.F = F;
   a.G = G;
+  HIPCHK(e->ensure_xml((size_t)a.total));
+  a.xml = e->xml;
   HIPCHK(launch_rows(a, (hipStream_t)stream));
   return MV_OK;
 }
@@ -458,6 +494,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   ev.hist_rows = hist_rows;
   ev.hist_w = hist_w;
   ev.hist_row0 = 0;
+  HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
+  ev.xml = e->xml;
   HIPCHK(launch_rows(ev, stream));
   SurvArgs sa{};
   sa.n_survive = P;
@@ -485,6 +523,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   HIPCHK(launch_survive(sa, B, stream));
   if (e->profiling) {
     if (ensure_events(e->ev_var, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
+    if (ensure_events(e->ev_mlp, (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_surv, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
   }
   e->n_var_rec = 0;
@@ -504,13 +543,16 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_rows = hist_rows;
   va.hist_w = hist_w;
   va.seed = prm->seed;
+  va.xml = e->xml;
   sa.N = P + O;
   for (int g = 1; g < G; ++g) {
     va.gen = g;
     va.hist_row0 = P + (g - 1) * O;
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], stream));
-    HIPCHK(launch_rows(va, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec++ + 1], stream));
+    HIPCHK(launch_vary(va, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], stream));
+    HIPCHK(launch_mlp(va, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], stream));
     sa.gen = g;
     sa.parents_out = g + 1 < G ? e->parents : nullptr;
     sa.sel_gen = g + 1;
@@ -521,15 +563,17 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   return MV_OK;
 }
 
-int mv_get_kernel_times(mv_engine* e, double* vareval_ms, double* survive_ms, int32_t* n_vareval,
-                        int32_t* n_survive) {
+int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
+                        int32_t* n_generations) {
   if (!e) return fail(MV_ERR_ARG, "null engine");
-  double tv = 0.0, ts = 0.0;
+  double tv = 0.0, tm = 0.0, ts = 0.0;
   for (int i = 0; i < e->n_var_rec; ++i) {
-    float ms = 0.f;
-    HIPCHK(hipEventSynchronize(e->ev_var[2 * i + 1]));
+    float ms = 0.f, ms2 = 0.f;
+    HIPCHK(hipEventSynchronize(e->ev_mlp[i]));
     HIPCHK(hipEventElapsedTime(&ms, e->ev_var[2 * i], e->ev_var[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&ms2, e->ev_var[2 * i + 1], e->ev_mlp[i]));
     tv += ms;
+    tm += ms2;
   }
   for (int i = 0; i < e->n_surv_rec; ++i) {
     float ms = 0.f;
@@ -537,10 +581,10 @@ int mv_get_kernel_times(mv_engine* e, double* vareval_ms, double* survive_ms, in
     HIPCHK(hipEventElapsedTime(&ms, e->ev_surv[2 * i], e->ev_surv[2 * i + 1]));
     ts += ms;
   }
-  if (vareval_ms) *vareval_ms = tv;
+  if (vary_ms) *vary_ms = tv;
+  if (mlp_ms) *mlp_ms = tm;
   if (survive_ms) *survive_ms = ts;
-  if (n_vareval) *n_vareval = e->n_var_rec;
-  if (n_survive) *n_survive = e->n_surv_rec;
+  if (n_generations) *n_generations = e->n_var_rec < e->n_surv_rec ? e->n_var_rec : e->n_surv_rec;
   return MV_OK;
 }
 

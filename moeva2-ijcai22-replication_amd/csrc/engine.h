@@ -29,11 +29,14 @@ struct DProblem {
   const int* gene_kind;   // [V]
   const int* gene_feat;   // [V]
   const int* gene_sub;    // [V] index within its subset
+  const int* gene_info;   // [V4] kind | sub << 2 | feat << 17 (zero padded to a multiple of 4)
   const int* ohe_off;     // [n_ohe+1]
   const int* ohe_feat;
   const int* mut_feat;    // [Dm]
   const double* ml_scale; // [D]
   const double* ml_min;   // [D]
+  const double* mlS;      // [Dm4] ml_scale gathered at the mutable features
+  const double* mlM;      // [Dm4] ml_min   gathered at the mutable features
   const int* op_code;     // [C]
   const int* op_arg;      // [C*4]
   const double* op_k;     // [C*2]
@@ -87,6 +90,7 @@ struct RowsArgs {
   double eta;               // 20
   double cx_prob;           // 0.9
   int do_eval;              // 0: variation only
+  float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
 };
 
 // Survival ------------------------------------------------------------------------------

@@ -1,20 +1,18 @@
 // Fitness evaluation and variation kernels (gfx950).
 //
-// k_rows: one workgroup = 32 candidate rows (flattened over (state, row)), 4 waves.
-//   Phase A (one wave per row, 8 rows per wave):
+// One generation's candidate rows go through two kernels:
+//  k_vary (one wave per row, small LDS, high occupancy):
 //     [mode 1] two-point crossover + polynomial mutation of the row's parents
 //              (moeva2.py:90-111 -> softmax_crossover.py:17-38 / softmax_mutation.py:20-67
 //              semantics, Philox draws), child written to the population pool;
-//     decode genes -> ML row x_f in LDS (feature_encoder.py:91-124),
-//     encoder MinMax distance f2 (default_problem.py:80-91, utils.py:11-22),
-//     ML-scaled fp32 A-tile row (default_problem.py:119-121),
-//     constraint program -> G, f3 (default_problem.py:93-97,128-129).
-//   Phase B: Dense-ReLU chain on MFMA (v_mfma_f32_16x16x4_f32, exact fp32 fma chains),
-//     layer 1 over the mutable columns only (immutable columns folded into a per-state
-//     bias), final Dense + softmax on the VALU (classifier.py:23-29).
-//   Phase C: F row (f1, f2, f3) + optional history row.
-// k_variation: phase A gene generation only (C-ABI mv_variation).
-// k_setup_states: per-state constants (mv_set_states).
+//     decode genes -> ML row x_f in LDS (feature_encoder.py:91-124);
+//     encoder MinMax distance f2 (default_problem.py:80-91, utils.py:11-22);
+//     constraint program -> G, f3 (default_problem.py:93-97,128-129);
+//     ML-scaled fp32 row (default_problem.py:119-121) -> scratch xml[row][Dm4].
+//  k_mlp (32-row tiles): the Dense-ReLU chain on MFMA (v_mfma_f32_16x16x4_f32, exact fp32
+//     fma chains), layer 1 over the mutable columns only (immutable columns folded into a
+//     per-state bias), final Dense + softmax on the VALU (classifier.py:23-29) -> f1.
+// k_predict: Classifier.predict_proba on ML rows.   k_setup_states: per-state constants.
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
@@ -176,47 +174,20 @@ __device__ __forceinline__ Cx cx_draws(const Rng& rng, int gen, int m, const int
   return c;
 }
 
-// Child gene g of offspring i (parents own/oth), crossover + mutation.
-__device__ __forceinline__ double child_gene(const RowsArgs& a, const Rng& rng, const Cx& cx,
-                                             const double* __restrict__ gown,
-                                             const double* __restrict__ goth, int b, int i, int g,
-                                             uint32_t word) {
-  const DProblem& p = a.p;
-  const int kind = p.gene_kind[g];
-  const int ss = kind == 0 ? 0 : 1;
-  const int sub = p.gene_sub[g];
-  const bool swap = cx.on[ss] && sub >= cx.lo[ss] && sub < cx.hi[ss];
-  double x = swap ? goth[g] : gown[g];
-  if (word < a.mut_thr) {
-    const u32x4 wu = rng.draw((uint32_t)(i * p.V + g), (uint32_t)a.gen, TAG_MUT_U);
-    const double u = u53(wu.x, wu.y);
-    const double xl = a.s.gl[(size_t)b * p.V + g];
-    const double xu = a.s.gu[(size_t)b * p.V + g];
-    if (kind == 0) {
-      x = poly_mut(x, xl, xu, u, a.eta);
-    } else {
-      double y = poly_mut(x, xl - INT_WIDEN, xu + INT_WIDEN, u, a.eta);
-      y = rint(y);  // np.round: half to even
-      if (y < xl) y = xl;
-      if (y > xu) y = xu;
-      x = y;
-    }
-  }
-  return x;
-}
-
-__device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restrict__ xrow, int g,
-                                             double x) {
-  if (p.gene_kind[g] != 2) {
-    xrow[p.gene_feat[g]] = x;
+__device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restrict__ xrow,
+                                             int info, double x) {
+  const int kind = info & 3;
+  const int feat = (info >> 17) & 0x7FFF;
+  if (kind != 2) {
+    xrow[feat] = x;
   } else {
-    const int q = p.gene_feat[g];
-    const int o0 = p.ohe_off[q], o1 = p.ohe_off[q + 1];
+    const int o0 = p.ohe_off[feat], o1 = p.ohe_off[feat + 1];
     for (int k = o0; k < o1; ++k) xrow[p.ohe_feat[k]] = (x == (double)(k - o0)) ? 1.0 : 0.0;
   }
 }
 
 // Generate (mode 1) or load (mode 0) the genes of row (b, i); lane-parallel, 4 genes/lane.
+// gene_info packs kind (2 bits) | subset index << 2 | feature (or OHE group) << 17.
 __device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xrow) {
   const DProblem& p = a.p;
   const int V = p.V;
@@ -230,7 +201,7 @@ __device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xro
     for (int g = lane; g < V; g += 64) {
       const double x = gin[g];
       if (gout) gout[g] = x;
-      if (xrow) scatter_gene(p, xrow, g, x);
+      if (xrow) scatter_gene(p, xrow, p.gene_info[g], x);
     }
     return;
   }
@@ -245,17 +216,46 @@ __device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xro
   const double* goth = a.genes_in + ((size_t)b * a.in_rows + oth) * V;
   const Cx cx = cx_draws(rng, a.gen, m, p.n_sub, a.cx_prob);
   const int nq = (V + 3) >> 2;
+  const double* gl = a.s.gl + (size_t)b * V;
+  const double* gu = a.s.gu + (size_t)b * V;
   for (int g0 = lane * 4; g0 < V; g0 += 256) {
+    const int4 inf4 = *(const int4*)(p.gene_info + g0);  // padded to a multiple of 4
     const u32x4 w = rng.draw((uint32_t)(i * nq + (g0 >> 2)), (uint32_t)a.gen, TAG_MUT_MASK);
+    double xv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int info = j == 0 ? inf4.x : (j == 1 ? inf4.y : (j == 2 ? inf4.z : inf4.w));
+      const int kind = info & 3;
+      const int ss = kind == 0 ? 0 : 1;
+      const int sub = (info >> 2) & 0x7FFF;
+      const bool swap = cx.on[ss] && sub >= cx.lo[ss] && sub < cx.hi[ss];
+      const double* src = swap ? goth : gown;
+      xv[j] = (g0 + j < V) ? src[g0 + j] : 0.0;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int g = g0 + j;
-      if (g < V) {
-        const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
-        const double x = child_gene(a, rng, cx, gown, goth, b, i, g, word);
-        if (gout) gout[g] = x;
-        if (xrow) scatter_gene(p, xrow, g, x);
+      if (g >= V) break;
+      const int info = j == 0 ? inf4.x : (j == 1 ? inf4.y : (j == 2 ? inf4.z : inf4.w));
+      const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
+      double x = xv[j];
+      if (word < a.mut_thr) {
+        const int kind = info & 3;
+        const u32x4 wu = rng.draw((uint32_t)(i * V + g), (uint32_t)a.gen, TAG_MUT_U);
+        const double u = u53(wu.x, wu.y);
+        const double xl = gl[g], xu = gu[g];
+        if (kind == 0) {
+          x = poly_mut(x, xl, xu, u, a.eta);
+        } else {
+          double y = poly_mut(x, xl - INT_WIDEN, xu + INT_WIDEN, u, a.eta);
+          y = rint(y);  // np.round: half to even
+          if (y < xl) y = xl;
+          if (y > xu) y = xu;
+          x = y;
+        }
       }
+      if (gout) gout[g] = x;
+      if (xrow) scatter_gene(p, xrow, info, x);
     }
   }
 }
@@ -324,8 +324,101 @@ __device__ __forceinline__ int max_hidden(const DProblem& p) {
   return h;
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Variation (mode 1) / gene load (mode 0) + decode + f2 + constraints/f3 + fp32 ML row.
+// One wave per row, 4 rows per workgroup; LDS = 4 ML rows (fp64).
+__global__ __launch_bounds__(256) void k_vary(RowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const DProblem& p = a.p;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= a.total) return;
+  const int b = r / a.n;
+  const int i = r - b * a.n;
+  double* xrow = (double*)smem + (size_t)wave * p.D;
+  if (!a.do_eval) {
+    row_genes(a, b, i, lane, nullptr);
+    return;
+  }
+  const double* xi = a.s.x_init + (size_t)b * p.D;
+#pragma unroll 4
+  for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
+  wave_sync();
+  row_genes(a, b, i, lane, xrow);
+  wave_sync();
+  // fp32 ML row (scratch) + encoder MinMax distance over the mutable features
+  const double* es = a.s.enc_scale + (size_t)b * p.Dm;
+  const double* em = a.s.enc_min + (size_t)b * p.Dm;
+  const double* x0 = a.s.x0_mm + (size_t)b * p.Dm;
+  float* xo = a.xml + (size_t)r * p.Dm4;
+  double acc = 0.0;
+#pragma unroll 2
+  for (int j = lane; j < p.Dm4; j += 64) {
+    float v = 0.f;
+    if (j < p.Dm) {
+      const double xf = xrow[p.mut_feat[j]];
+      v = (float)(xf * p.mlS[j] + p.mlM[j]);
+      const double d = (xf * es[j] + em[j]) - x0[j];
+      if (p.norm == 2)
+        acc += d * d;
+      else
+        acc = nanmax(acc, fabs(d));
+    }
+    xo[j] = v;
+  }
+  acc = p.norm == 2 ? wave_sum(acc) : wave_max(acc);
+  double f2 = p.norm == 2 ? sqrt(acc) : acc;
+  if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
+  // constraint program
+  double acc3 = 0.0;
+  double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+  double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows + a.hist_row0 + i) * a.hist_w : nullptr;
+  const bool hfull = hrow && a.hist_w > 3;
+#pragma unroll 2
+  for (int c = lane; c < p.C; c += 64) {
+    if (p.op_code[c] == 3) continue;  // ABS_SUMDIFF: wave-parallel below
+    double v = eval_op(p, c, xrow);
+    if (v <= p.tol) v = 0.0;
+    const double g = v * (v > 0.0 ? 1.0 : 0.0);
+    if (grow) grow[c] = g;
+    if (hfull) hrow[3 + c] = g;
+    acc3 += g;
+  }
+  for (int k = 0; k < p.n_sumdiff; ++k) {
+    const int c = p.sumdiff_ops[k];
+    double v = sumdiff_wave(p, c, xrow, lane);
+    if (v <= p.tol) v = 0.0;
+    const double g = v * (v > 0.0 ? 1.0 : 0.0);
+    if (lane == 0) {
+      if (grow) grow[c] = g;
+      if (hfull) hrow[3 + c] = g;
+      acc3 += g;
+    }
+  }
+  acc3 = wave_sum(acc3);
+  if (lane == 0) {
+    if (a.F) {
+      const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
+      double* fr = a.F + ((size_t)b * a.out_rows + orow) * 3;
+      fr[1] = f2;
+      fr[2] = acc3;
+    }
+    if (hrow) {
+      hrow[1] = f2;
+      hrow[2] = acc3;
+    }
+  }
+}
+
+// Dense chain over 32-row tiles of the fp32 ML rows -> f1.
 template <int MAXCT>
-__global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
+__global__ __launch_bounds__(EVAL_T) void k_mlp(RowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const DProblem& p = a.p;
   const int tid = threadIdx.x;
@@ -333,106 +426,29 @@ __global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
   const int wave = tid >> 6;
   const int lda = p.Dm4 + 1;
   const int hmax = max_hidden(p);
-  // LDS carve (kept in sync with eval_lds_bytes)
-  int* row_state = (int*)smem;                       // [32]
-  int* row_idx = row_state + EVAL_TR;                // [32]
-  double* row_f2 = (double*)(row_idx + EVAL_TR);     // [32]
-  double* row_f3 = row_f2 + EVAL_TR;                 // [32]
-  unsigned char* base = (unsigned char*)(row_f3 + EVAL_TR);
-  const size_t r1 = eval_region1_bytes(p.Dm4, hmax);
-  float* R1 = (float*)base;
-  unsigned char* R2 = base + r1;
+  int* row_state = (int*)smem;  // [32]
+  const size_t head = 256;
+  float* R1 = (float*)(smem + head);
+  float* R2 = (float*)(smem + head + eval_region1_bytes(p.Dm4, hmax));
   const int r0 = blockIdx.x * EVAL_TR;
-
-  // ---------------- Phase A
-  for (int rr = 0; rr < EVAL_TR / 4; ++rr) {
-    const int t = rr * 4 + wave;
+  if (tid < EVAL_TR) row_state[tid] = (r0 + tid < a.total) ? (r0 + tid) / a.n : -1;
+  const int nq = p.Dm4 >> 2;
+  for (int idx = tid; idx < EVAL_TR * nq; idx += EVAL_T) {
+    const int t = idx / nq, q = idx - t * nq;
     const int r = r0 + t;
-    const bool valid = r < a.total;
-    double* xrow = (double*)R2 + (size_t)wave * p.D;
-    int b = 0, i = 0;
-    if (valid) {
-      b = r / a.n;
-      i = r - b * a.n;
-      const double* xi = a.s.x_init + (size_t)b * p.D;
-      for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
-    }
-    __syncthreads();
-    if (valid) row_genes(a, b, i, lane, xrow);
-    __syncthreads();
-    float* arow = R1 + t * lda;
-    if (valid) {
-      const double* es = a.s.enc_scale + (size_t)b * p.Dm;
-      const double* em = a.s.enc_min + (size_t)b * p.Dm;
-      const double* x0 = a.s.x0_mm + (size_t)b * p.Dm;
-      double acc = 0.0;
-      for (int j = lane; j < p.Dm4; j += 64) {
-        float v = 0.f;
-        if (j < p.Dm) {
-          const int f = p.mut_feat[j];
-          const double xf = xrow[f];
-          const double xm = xf * p.ml_scale[f] + p.ml_min[f];
-          v = (float)xm;
-          const double mm = xf * es[j] + em[j];
-          const double d = mm - x0[j];
-          if (p.norm == 2)
-            acc += d * d;
-          else
-            acc = nanmax(acc, fabs(d));
-        }
-        arow[j] = v;
-      }
-      acc = p.norm == 2 ? wave_sum(acc) : wave_max(acc);
-      double f2 = p.norm == 2 ? sqrt(acc) : acc;
-      if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-      double acc3 = 0.0;
-      double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-      double* hrow = (a.hist && a.hist_w > 3)
-                         ? a.hist + ((size_t)b * a.hist_rows + a.hist_row0 + i) * a.hist_w + 3
-                         : nullptr;
-      for (int c = lane; c < p.C; c += 64) {
-        if (p.op_code[c] == 3) continue;  // ABS_SUMDIFF: wave-parallel below
-        double v = eval_op(p, c, xrow);
-        if (v <= p.tol) v = 0.0;
-        const double g = v * (v > 0.0 ? 1.0 : 0.0);
-        if (grow) grow[c] = g;
-        if (hrow) hrow[c] = g;
-        acc3 += g;
-      }
-      for (int k = 0; k < p.n_sumdiff; ++k) {
-        const int c = p.sumdiff_ops[k];
-        double v = sumdiff_wave(p, c, xrow, lane);
-        if (v <= p.tol) v = 0.0;
-        const double g = v * (v > 0.0 ? 1.0 : 0.0);
-        if (lane == 0) {
-          if (grow) grow[c] = g;
-          if (hrow) hrow[c] = g;
-          acc3 += g;
-        }
-      }
-      acc3 = wave_sum(acc3);
-      if (lane == 0) {
-        row_state[t] = b;
-        row_idx[t] = i;
-        row_f2[t] = f2;
-        row_f3[t] = acc3;
-      }
-    } else {
-      for (int j = lane; j < p.Dm4; j += 64) arow[j] = 0.f;
-      if (lane == 0) {
-        row_state[t] = -1;
-        row_idx[t] = 0;
-      }
-    }
-    __syncthreads();
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < a.total) v = *(const float4*)(a.xml + (size_t)r * p.Dm4 + 4 * q);
+    float* d = R1 + t * lda + 4 * q;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
   }
-  if (!a.do_eval) return;
-
-  // ---------------- Phase B: Dense chain
+  __syncthreads();
   const float* in = R1;
   int ldi = lda;
   int K = p.Dm4;
-  float* outb = (float*)R2;
+  float* outb = R2;
   float* other = R1;
   for (int l = 0; l + 1 < p.n_layers; ++l) {
     const int N = p.dims[l + 1];
@@ -447,7 +463,6 @@ __global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
     outb = other;
     other = tmp;
   }
-  // final Dense + softmax (VALU), one thread per row
   if (tid < EVAL_TR) {
     const int t = tid;
     const int st = row_state[t];
@@ -469,22 +484,13 @@ __global__ __launch_bounds__(EVAL_T) void k_rows(RowsArgs a) {
         logit[c] = expf(logit[c] - mx);
         den += logit[c];
       }
-      const int mc = a.s.min_class[st];
-      const double f1 = (double)(logit[mc] / den);
-      const int i = row_idx[t];
+      const double f1 = (double)(logit[a.s.min_class[st]] / den);
+      const int i = (r0 + t) - st * a.n;
       if (a.F) {
         const int orow = a.out_map ? a.out_map[(size_t)st * a.n + i] : i;
-        double* fr = a.F + ((size_t)st * a.out_rows + orow) * 3;
-        fr[0] = f1;
-        fr[1] = row_f2[t];
-        fr[2] = row_f3[t];
+        a.F[((size_t)st * a.out_rows + orow) * 3] = f1;
       }
-      if (a.hist) {
-        double* hr = a.hist + ((size_t)st * a.hist_rows + a.hist_row0 + i) * a.hist_w;
-        hr[0] = f1;
-        hr[1] = row_f2[t];
-        hr[2] = row_f3[t];
-      }
+      if (a.hist) a.hist[((size_t)st * a.hist_rows + a.hist_row0 + i) * a.hist_w] = f1;
     }
   }
 }
@@ -569,16 +575,6 @@ __global__ __launch_bounds__(256) void k_constraints(DProblem p, int n, const do
   }
 }
 
-// Variation only: one wave per offspring row.
-__global__ __launch_bounds__(256) void k_variation(RowsArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.total) return;
-  const int b = r / a.n;
-  const int i = r - b * a.n;
-  row_genes(a, b, i, lane, nullptr);
-}
-
 // Per-state constants: one workgroup per state.
 __global__ __launch_bounds__(256) void k_setup_states(DProblem p, int B, const double* x_init,
                                                       const double* xl, const double* xu,
@@ -656,10 +652,11 @@ static void configure_lds_once() {
   static bool done = false;
   if (done) return;
   const int lim = 160 * 1024;
-  (void)hipFuncSetAttribute((const void*)k_rows<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_rows<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_rows<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_rows<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_mlp<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_mlp<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_mlp<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_mlp<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  (void)hipFuncSetAttribute((const void*)k_vary, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
   (void)hipFuncSetAttribute((const void*)k_predict<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
   (void)hipFuncSetAttribute((const void*)k_predict<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
   (void)hipFuncSetAttribute((const void*)k_predict<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -669,25 +666,37 @@ static void configure_lds_once() {
   done = true;
 }
 
-hipError_t launch_rows(const RowsArgs& a, hipStream_t stream) {
+hipError_t launch_vary(const RowsArgs& a, hipStream_t stream) {
+  if (a.total <= 0) return hipSuccess;
+  configure_lds_once();
+  const size_t lds = a.do_eval ? (size_t)4 * a.p.D * sizeof(double) : 0;
+  hipLaunchKernelGGL(k_vary, dim3((a.total + 3) / 4), dim3(256), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_mlp(const RowsArgs& a, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
   configure_lds_once();
   int hmax = 16;
   for (int l = 1; l < a.p.n_layers; ++l) hmax = a.p.dims[l] > hmax ? a.p.dims[l] : hmax;
-  const size_t lds = eval_lds_bytes(a.p.D, a.p.Dm4, hmax);
+  const size_t lds = mlp_lds_bytes(a.p.Dm4, hmax);
   const int grid = (a.total + EVAL_TR - 1) / EVAL_TR;
-  int maxn = 16;
-  for (int l = 1; l < a.p.n_layers; ++l) maxn = a.p.dims[l] > maxn ? a.p.dims[l] : maxn;
-  const int nct = maxn / 16;
+  const int nct = hmax / 16;
   if (nct <= 4)
-    hipLaunchKernelGGL(k_rows<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
   else if (nct <= 8)
-    hipLaunchKernelGGL(k_rows<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
   else if (nct <= 16)
-    hipLaunchKernelGGL(k_rows<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
   else
-    hipLaunchKernelGGL(k_rows<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
   return hipGetLastError();
+}
+
+hipError_t launch_rows(const RowsArgs& a, hipStream_t stream) {
+  hipError_t e = launch_vary(a, stream);
+  if (e != hipSuccess || !a.do_eval) return e;
+  return launch_mlp(a, stream);
 }
 
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream) {
@@ -719,9 +728,9 @@ hipError_t launch_constraints(const DProblem& p, int n, const double* x, double*
 }
 
 hipError_t launch_variation(const RowsArgs& a, hipStream_t stream) {
-  if (a.total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_variation, dim3((a.total + 3) / 4), dim3(256), 0, stream, a);
-  return hipGetLastError();
+  RowsArgs v = a;
+  v.do_eval = 0;
+  return launch_vary(v, stream);
 }
 
 hipError_t launch_setup_states(const DProblem& p, int B, const double* x_init, const double* xl,

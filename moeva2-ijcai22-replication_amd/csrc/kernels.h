@@ -22,9 +22,15 @@ __host__ __device__ inline size_t eval_lds_bytes(int D, int Dm4, int hmax) {
 }
 
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
+__host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax) {
+  return 256 + eval_region1_bytes(Dm4, hmax) + (size_t)EVAL_TR * (hmax + 1) * sizeof(float);
+}
+
 size_t surv_lds_bytes(int N, int R, int P);
 
 hipError_t launch_rows(const RowsArgs& a, hipStream_t stream);
+hipError_t launch_vary(const RowsArgs& a, hipStream_t stream);
+hipError_t launch_mlp(const RowsArgs& a, hipStream_t stream);
 hipError_t launch_constraints(const DProblem& p, int n, const double* x, double* G,
                               hipStream_t stream);
 hipError_t launch_variation(const RowsArgs& a, hipStream_t stream);

@@ -88,7 +88,7 @@ def lib():
             "mv_attack_population": [vp, vp, vp, vp],
             "mv_attack_history": [vp, vp, vp],
             "mv_set_profiling": [vp, C.c_int32],
-            "mv_get_kernel_times": [vp, _f64p, _f64p, _i32p, _i32p],
+            "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
         }
@@ -208,6 +208,7 @@ class Engine:
         check(L.mv_engine_create(device, C.byref(pd), C.byref(md) if weights is not None else None,
                                  C.byref(self._h)))
         self.B = 0
+        self.dims = dims if weights is not None else []
         self.n_out = dims[-1] if weights is not None else 0
 
     def __del__(self):
@@ -259,12 +260,13 @@ class Engine:
         check(lib().mv_set_profiling(self._h, int(on)))
 
     def kernel_times(self):
-        tv, ts = C.c_double(), C.c_double()
-        nv, ns = C.c_int32(), C.c_int32()
-        check(lib().mv_get_kernel_times(self._h, C.byref(tv), C.byref(ts), C.byref(nv),
-                                        C.byref(ns)))
-        return {"vareval_ms": tv.value, "survive_ms": ts.value, "n_vareval": nv.value,
-                "n_survive": ns.value}
+        """Summed device ms of k_vary / k_mlp / k_survive over the last profiled attack."""
+        tv, tm, ts = C.c_double(), C.c_double(), C.c_double()
+        n = C.c_int32()
+        check(lib().mv_get_kernel_times(self._h, C.byref(tv), C.byref(tm), C.byref(ts),
+                                        C.byref(n)))
+        return {"vary_ms": tv.value, "mlp_ms": tm.value, "survive_ms": ts.value,
+                "generations": n.value}
 
 
 def survive(F, ref_points, n_survive, mu, seed, gen, ideal, worst, extreme, has_extreme,
