@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -84,6 +85,7 @@ struct mv_engine {
   double* hist = nullptr;
   bool attack_ready = false;
   bool has_model = false;
+  long long* d_phase = nullptr;  // MV_SURV_PHASES=1: survival phase clocks [B][16]
   float* xml = nullptr;  // k_vary -> k_mlp scratch
   size_t xml_cap = 0;
   hipError_t ensure_xml(size_t rows) {
@@ -120,6 +122,7 @@ struct mv_engine {
     for (auto e : ev_var) (void)hipEventDestroy(e);
     for (auto e : ev_mlp) (void)hipEventDestroy(e);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
+    (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
 };
 
@@ -222,6 +225,10 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   for (int c = 0; c < C; ++c)
     if (pd->op_code[c] == MV_OP_ABS_SUMDIFF) sdo.push_back(c);
   p.n_sumdiff = (int)sdo.size();
+  p.full_ops = 0;
+  for (int c = 0; c < C; ++c)
+    if (pd->op_code[c] >= MV_OP_LCLD_INSTALL && pd->op_code[c] <= MV_OP_RATIO_MASKED)
+      p.full_ops = 1;
   K((int**)&p.sumdiff_ops, sdo.data(), sdo.size());
   p.tol = pd->tol;
   p.norm = pd->norm;
@@ -256,18 +263,24 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     delete e;
     return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
   }
-  int hmax = 16;
-  for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
-  const size_t lds = mlp_lds_bytes(p.Dm4, hmax);
-  if (md && (lds > 160 * 1024 || (size_t)4 * D * 8 > 160 * 1024)) {
-    delete e;
-    return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
+  if (md) {
+    int hmax = 16;
+    for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
+    const size_t lds = mlp_lds_bytes(p.Dm4, hmax, p.dims[p.n_layers - 1], p.dims[p.n_layers]);
+    const size_t lds_pred = mlp_lds_bytes((D + 3) & ~3, hmax, p.dims[p.n_layers - 1],
+                                          p.dims[p.n_layers]);
+    if (lds > 160 * 1024 || lds_pred > 160 * 1024) {
+      delete e;
+      return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
+    }
   }
   *out = e;
   return MV_OK;
 }
 
 void mv_engine_destroy(mv_engine* e) { delete e; }
+
+static RowsArgs base_rows(const mv_engine* e);
 
 int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* xl,
                   const double* xu, const int32_t* minimize_class, void* stream) {
@@ -282,6 +295,7 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
   HIPCHK(hipDeviceSynchronize());
   e->free_list(e->state_allocs);
   e->free_list(e->attack_allocs);
+  e->d_phase = nullptr;
   e->attack_ready = false;
   const DProblem& p = e->p;
   DStates& s = e->s;
@@ -303,9 +317,12 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
   K((float**)&s.bias1, (const float*)nullptr, (size_t)B * e->H1);
   K(&e->genes0, (const double*)nullptr, (size_t)B * p.V);
   if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
-  HIPCHK(launch_setup_states(p, B, s.x_init, dxl, dxu, e->W1full, e->b1, (double*)s.gl,
+  int slot = 0;
+  HIPCHK(stage_rows(base_rows(e), (hipStream_t)stream, &slot));
+  HIPCHK(launch_setup_states(slot, B, s.x_init, dxl, dxu, e->W1full, e->b1, (double*)s.gl,
                              (double*)s.gu, (double*)s.enc_scale, (double*)s.enc_min,
                              (double*)s.x0_mm, (float*)s.bias1, e->genes0, (hipStream_t)stream));
+  HIPCHK(release_rows(slot, (hipStream_t)stream));
   e->B = B;
   return MV_OK;
 }
@@ -336,14 +353,20 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
   a.G = G;
   HIPCHK(e->ensure_xml((size_t)a.total));
   a.xml = e->xml;
-  HIPCHK(launch_rows(a, (hipStream_t)stream));
+  int slot = 0;
+  HIPCHK(stage_rows(a, (hipStream_t)stream, &slot));
+  HIPCHK(launch_rows(a, slot, 0, 0, (hipStream_t)stream));
+  HIPCHK(release_rows(slot, (hipStream_t)stream));
   return MV_OK;
 }
 
 int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream) {
   if (!e || n < 0 || (n > 0 && (!x || !G))) return fail(MV_ERR_ARG, "bad mv_constraints arguments");
   HIPCHK(hipSetDevice(e->device));
-  HIPCHK(launch_constraints(e->p, n, x, G, (hipStream_t)stream));
+  int slot = 0;
+  HIPCHK(stage_rows(base_rows(e), (hipStream_t)stream, &slot));
+  HIPCHK(launch_constraints(e->p, slot, n, x, G, (hipStream_t)stream));
+  HIPCHK(release_rows(slot, (hipStream_t)stream));
   return MV_OK;
 }
 
@@ -363,9 +386,11 @@ int mv_variation(mv_engine* e, int32_t P, int32_t O, uint64_t seed, int32_t gen,
   a.genes_out = off;
   a.out_rows = O;
   a.seed = seed;
-  a.gen = gen;
   a.do_eval = 0;
-  HIPCHK(launch_variation(a, (hipStream_t)stream));
+  int slot = 0;
+  HIPCHK(stage_rows(a, (hipStream_t)stream, &slot));
+  HIPCHK(launch_vary(a, slot, gen, 0, (hipStream_t)stream));
+  HIPCHK(release_rows(slot, (hipStream_t)stream));
   return MV_OK;
 }
 
@@ -405,6 +430,11 @@ int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t
 int mv_select_parents(int32_t B, int32_t P, int32_t O, uint64_t seed, int32_t gen,
                       int32_t* parents, void* stream) {
   if (B <= 0 || P <= 1 || O <= 0 || !parents) return fail(MV_ERR_ARG, "bad mv_select_parents");
+  const int n_m = (O + 1) / 2, slots = ((n_m * 4 + P - 1) / P) * P;
+  int p2 = 1;
+  while (p2 < slots) p2 <<= 1;
+  if (P > 8192 || (size_t)p2 * 8 + (size_t)slots * 4 > 160 * 1024)
+    return fail(MV_ERR_ARG, "mv_select_parents: population or offspring count too large");
   HIPCHK(launch_select(B, P, O, seed, 0u, gen, nullptr, parents, (hipStream_t)stream));
   return MV_OK;
 }
@@ -443,6 +473,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   if (realloc) {
     HIPCHK(hipDeviceSynchronize());
     e->free_list(e->attack_allocs);
+    e->d_phase = nullptr;
     hipError_t err = hipSuccess;
     auto A = [&](auto** dst, size_t n) {
       if (err != hipSuccess) return;
@@ -493,10 +524,12 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   ev.hist = prm->history ? e->hist : nullptr;
   ev.hist_rows = hist_rows;
   ev.hist_w = hist_w;
-  ev.hist_row0 = 0;
   HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
   ev.xml = e->xml;
-  HIPCHK(launch_rows(ev, stream));
+  int slot_ev = 0;
+  HIPCHK(stage_rows(ev, stream, &slot_ev));
+  HIPCHK(launch_rows(ev, slot_ev, 0, 0, stream));
+  HIPCHK(release_rows(slot_ev, stream));
   SurvArgs sa{};
   sa.n_survive = P;
   sa.P = P;
@@ -515,6 +548,13 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.extreme = e->extreme;
   sa.has_extreme = e->has_ext;
   sa.O_next = O;
+  if (std::getenv("MV_SURV_PHASES")) {
+    if (!e->d_phase) {
+      HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 16 * sizeof(long long)));
+      e->attack_allocs.push_back(e->d_phase);
+    }
+    sa.phase = e->d_phase;
+  }
   // dummy survival at initialisation: n_survive == len(pop)
   sa.N = P;
   sa.gen = 0;
@@ -544,14 +584,15 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_w = hist_w;
   va.seed = prm->seed;
   va.xml = e->xml;
+  int slot_va = 0;
+  HIPCHK(stage_rows(va, stream, &slot_va));
   sa.N = P + O;
   for (int g = 1; g < G; ++g) {
-    va.gen = g;
-    va.hist_row0 = P + (g - 1) * O;
+    const int hist_row0 = P + (g - 1) * O;
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], stream));
-    HIPCHK(launch_vary(va, stream));
+    HIPCHK(launch_vary(va, slot_va, g, hist_row0, stream));
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], stream));
-    HIPCHK(launch_mlp(va, stream));
+    HIPCHK(launch_mlp(va, slot_va, hist_row0, stream));
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], stream));
     sa.gen = g;
     sa.parents_out = g + 1 < G ? e->parents : nullptr;
@@ -560,6 +601,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     HIPCHK(launch_survive(sa, B, stream));
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec++ + 1], stream));
   }
+  HIPCHK(release_rows(slot_va, stream));
   return MV_OK;
 }
 
@@ -585,6 +627,26 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
   if (mlp_ms) *mlp_ms = tm;
   if (survive_ms) *survive_ms = ts;
   if (n_generations) *n_generations = e->n_var_rec < e->n_surv_rec ? e->n_var_rec : e->n_surv_rec;
+  if (e->d_phase && e->B > 0) {  // development aid: survival phase split of the last generation
+    std::vector<long long> ph((size_t)e->B * 16);
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(ph.data(), e->d_phase, ph.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    double acc[16] = {0};
+    for (int b = 0; b < e->B; ++b)
+      for (int k = 1; k < 10; ++k) acc[k] += (double)(ph[(size_t)b * 16 + k] - ph[(size_t)b * 16 + k - 1]);
+    std::fprintf(stderr, "[mv] survival phase cycles (mean over %d states):", e->B);
+    for (int k = 1; k < 10; ++k) std::fprintf(stderr, " p%d=%.0f", k, acc[k] / e->B);
+    double red = 0.0, afast = 0.0, nflag = 0.0;
+    for (int b = 0; b < e->B; ++b) {
+      const long long* q = &ph[(size_t)b * 16];
+      red += (double)(q[11] - q[1]);
+      afast += (double)(q[10] - q[5]);
+      nflag += (double)q[12];
+    }
+    std::fprintf(stderr, " | ideal/worst=%.0f assoc_fast=%.0f flagged=%.1f", red / e->B,
+                 afast / e->B, nflag / e->B);
+    std::fprintf(stderr, "\n");
+  }
   return MV_OK;
 }
 

@@ -18,9 +18,10 @@ namespace mv {
 constexpr int MAX_LAYERS = 6;
 constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
 constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
-constexpr int SURV_T = 256;      // threads per survival workgroup
+constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
 constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS
 constexpr int SURV_RMAX = 640;   // reference points
+constexpr int ARG_SLOTS = 32;    // constant-memory launch-argument slots per device
 constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound widening
 
 struct DProblem {
@@ -42,6 +43,7 @@ struct DProblem {
   const double* op_k;     // [C*2]
   const int* idx_pool;
   int n_sumdiff;          // ABS_SUMDIFF ops, evaluated wave-parallel
+  int full_ops;           // program uses the LCLD financial ops (codes 4..8)
   const int* sumdiff_ops; // [n_sumdiff] their column indices
   double tol;
   int norm;               // 2 or 0 (inf)
@@ -82,9 +84,8 @@ struct RowsArgs {
   double* F;                // [B][out_rows][3] (rows follow out_map) or NULL
   double* G;                // [B][n][C] or NULL
   double* hist;             // [B][hist_rows][hist_w] or NULL
-  int hist_rows, hist_w, hist_row0;
+  int hist_rows, hist_w;
   uint64_t seed;
-  int gen;
   uint32_t stream_key;
   uint32_t mut_thr;         // floor(2^32 / V)
   double eta;               // 20
@@ -124,6 +125,7 @@ struct SurvArgs {
   int* parents_out;         // [B][n_m][2] (slots in slot mode, positions otherwise) or NULL
   int O_next;               // offspring of the next generation (selection)
   int sel_gen;
+  long long* phase;         // [B][16] clock64() at phase boundaries (development), or NULL
 };
 
 // Stand-alone classifier forward (Classifier.predict_proba) -------------------------------

@@ -10,14 +10,71 @@
 //     constraint program -> G, f3 (default_problem.py:93-97,128-129);
 //     ML-scaled fp32 row (default_problem.py:119-121) -> scratch xml[row][Dm4].
 //  k_mlp (32-row tiles): the Dense-ReLU chain on MFMA (v_mfma_f32_16x16x4_f32, exact fp32
-//     fma chains), layer 1 over the mutable columns only (immutable columns folded into a
-//     per-state bias), final Dense + softmax on the VALU (classifier.py:23-29) -> f1.
+//     products), layer 1 over the mutable columns only (immutable columns folded into a
+//     per-state bias), final Dense + softmax on the VALU with its weights in LDS
+//     (classifier.py:23-29) -> f1.
 // k_predict: Classifier.predict_proba on ML rows.   k_setup_states: per-state constants.
+//
+// Launch arguments live in constant memory: a ring of RowsArgs slots per device (c_rows),
+// written stream-ordered from pinned host copies.  As by-value kernel arguments the
+// several-hundred-byte structs spilled SGPRs into VGPRs; from a plain global buffer the
+// pointers they hold lose their address space (every access became a flat op); pointers
+// loaded from the constant address space are known to be global.  Only the
+// per-generation scalars (slot, gen, first history row) are passed by value.
+#include <mutex>
+
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
 
 namespace mv {
+
+__constant__ RowsArgs c_rows[ARG_SLOTS];
+
+namespace {
+struct ArgRing {
+  bool ready = false;
+  RowsArgs* host = nullptr;  // pinned [ARG_SLOTS]
+  hipEvent_t ev[ARG_SLOTS] = {};
+  int next = 0;
+};
+constexpr int MAX_DEVICES = 64;
+ArgRing g_rings[MAX_DEVICES];
+std::mutex g_ring_mu;
+}  // namespace
+
+hipError_t stage_rows(const RowsArgs& a, hipStream_t stream, int* slot) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= MAX_DEVICES) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lock(g_ring_mu);
+  ArgRing& r = g_rings[dev];
+  if (!r.ready) {
+    e = hipHostMalloc((void**)&r.host, ARG_SLOTS * sizeof(RowsArgs));
+    for (int i = 0; i < ARG_SLOTS && e == hipSuccess; ++i)
+      e = hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    r.ready = true;
+  }
+  const int k = r.next;
+  r.next = (r.next + 1) % ARG_SLOTS;
+  e = hipEventSynchronize(r.ev[k]);  // the slot's previous launches have finished
+  if (e != hipSuccess) return e;
+  r.host[k] = a;
+  e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_rows), r.host + k, sizeof(RowsArgs),
+                             (size_t)k * sizeof(RowsArgs), hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) *slot = k;
+  return e;
+}
+
+hipError_t release_rows(int slot, hipStream_t stream) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(g_ring_mu);
+  return hipEventRecord(g_rings[dev].ev[slot], stream);
+}
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -39,6 +96,12 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // numpy float remainder (npy_divmod): result takes the divisor's sign
 __device__ __forceinline__ double py_mod(double a, double b) {
   double m = fmod(a, b);
@@ -54,69 +117,103 @@ __device__ __forceinline__ double month_of(double f) {
   return floor(f / 100.0) * 12.0 + py_mod(f, 100.0);
 }
 
-// One constraint column on the ML row x (LDS).
-__device__ double eval_op(const DProblem& p, int c, const double* __restrict__ x) {
+// One constraint column on the ML row x (LDS).  FULL adds the LCLD financial identities;
+// ABS_SUMDIFF columns are evaluated wave-parallel (sumdiff_wave) by the caller.
+template <bool FULL>
+__device__ __forceinline__ double eval_op(const DProblem& p, int c, const double* __restrict__ x) {
   const int code = p.op_code[c];
-  const int* ar = p.op_arg + 4 * c;
-  const double* k = p.op_k + 2 * c;
+  const int4 ar = *(const int4*)(p.op_arg + 4 * c);
   switch (code) {
-    case 1:  // MV_OP_DIFF
-      return x[ar[0]] - x[ar[1]];
-    case 2: {  // MV_OP_RATIO_SAFE
-      const double a = x[ar[0]], b = x[ar[1]];
-      return (b != 0.0 ? a / b : 0.0) - k[0];
+    case 1:  // MV_OP_DIFF (botnet_constraints.py:283-285)
+      return x[ar.x] - x[ar.y];
+    case 2: {  // MV_OP_RATIO_SAFE (botnet_constraints.py:304-306)
+      const double a = x[ar.x], b = x[ar.y];
+      return (b != 0.0 ? a / b : 0.0) - p.op_k[2 * c];
     }
-    case 3: {  // MV_OP_ABS_SUMDIFF (integer-valued features in every shipped program)
-      double s0 = 0.0, s1 = 0.0;
-      for (int q = ar[0]; q < ar[1]; ++q) s0 += x[p.idx_pool[q]];
-      for (int q = ar[1]; q < ar[2]; ++q) s1 += x[p.idx_pool[q]];
-      return fabs(s0 - s1);
-    }
-    case 4: {  // MV_OP_LCLD_INSTALL (lcld_constraints.py:174-177), numpy evaluation order
-      const double x0 = x[ar[0]], x1 = x[ar[1]], x2 = x[ar[2]], x3 = x[ar[3]];
-      const double r = x2 / 1200.0;
-      const double base = 1.0 + x2 / 1200.0;
-      const double num = (x0 * r) * pow(base, x1);
-      const double den = pow(base, x1) - 1.0;
-      return fabs(x3 - num / den) - k[0];
-    }
-    case 5: {  // MV_OP_LCLD_TERM
-      const double t = x[ar[0]];
-      return fabs((36.0 - t) * (60.0 - t));
-    }
-    case 6:  // MV_OP_ABS_RATIO
-      return fabs(x[ar[0]] - x[ar[1]] / x[ar[2]]);
-    case 7:  // MV_OP_MONTHDIFF
-      return fabs(x[ar[0]] - (month_of(x[ar[1]]) - month_of(x[ar[2]])));
-    case 8: {  // MV_OP_RATIO_MASKED
-      const double den = x[ar[2]];
-      double ratio = -1.0;
-      if (den != 0.0) {
-        ratio = x[ar[1]] / den;
-        if (ratio == __builtin_inf() || ratio != ratio) ratio = -1.0;
-      }
-      return fabs(x[ar[0]] - ratio);
-    }
-    case 9: {  // MV_OP_XOR_AUG
-      const bool b1 = x[ar[1]] >= k[0];
-      const bool b2 = x[ar[2]] >= k[1];
-      return fabs(x[ar[0]] - ((b1 != b2) ? 1.0 : 0.0));
+    case 9: {  // MV_OP_XOR_AUG (examples/utils.py:7-29)
+      const double2 k = *(const double2*)(p.op_k + 2 * c);
+      const bool b1 = x[ar.y] >= k.x;
+      const bool b2 = x[ar.z] >= k.y;
+      return fabs(x[ar.x] - ((b1 != b2) ? 1.0 : 0.0));
     }
     default:
-      return __builtin_nan("");
+      break;
   }
+  if (FULL) {
+    switch (code) {
+      case 4: {  // MV_OP_LCLD_INSTALL (lcld_constraints.py:174-177), numpy evaluation order
+        const double x0 = x[ar.x], x1 = x[ar.y], x2 = x[ar.z], x3 = x[ar.w];
+        const double r = x2 / 1200.0;
+        const double base = 1.0 + x2 / 1200.0;
+        const double num = (x0 * r) * pow(base, x1);
+        const double den = pow(base, x1) - 1.0;
+        return fabs(x3 - num / den) - p.op_k[2 * c];
+      }
+      case 5: {  // MV_OP_LCLD_TERM (:186)
+        const double t = x[ar.x];
+        return fabs((36.0 - t) * (60.0 - t));
+      }
+      case 6:  // MV_OP_ABS_RATIO (:189-207)
+        return fabs(x[ar.x] - x[ar.y] / x[ar.z]);
+      case 7:  // MV_OP_MONTHDIFF (:195-201)
+        return fabs(x[ar.x] - (month_of(x[ar.y]) - month_of(x[ar.z])));
+      case 8: {  // MV_OP_RATIO_MASKED (:210-216)
+        const double den = x[ar.z];
+        double ratio = -1.0;
+        if (den != 0.0) {
+          ratio = x[ar.y] / den;
+          if (ratio == __builtin_inf() || ratio != ratio) ratio = -1.0;
+        }
+        return fabs(x[ar.x] - ratio);
+      }
+      default:
+        break;
+    }
+  }
+  return __builtin_nan("");
 }
 
 // |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes (exact for the integer-valued
 // features of every shipped program; summation order differs from numpy otherwise).
-__device__ __forceinline__ double sumdiff_wave(const DProblem& p, int c, const double* x, int lane) {
-  const int* ar = p.op_arg + 4 * c;
+__device__ __forceinline__ double sumdiff_wave(const DProblem& p, int c, const double* x,
+                                               int lane) {
+  const int4 ar = *(const int4*)(p.op_arg + 4 * c);
   double s0 = 0.0, s1 = 0.0;
-  for (int q = ar[0] + lane; q < ar[1]; q += 64) s0 += x[p.idx_pool[q]];
-  for (int q = ar[1] + lane; q < ar[2]; q += 64) s1 += x[p.idx_pool[q]];
+  for (int q = ar.x + lane; q < ar.y; q += 64) s0 += x[p.idx_pool[q]];
+  for (int q = ar.y + lane; q < ar.z; q += 64) s1 += x[p.idx_pool[q]];
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
   return fabs(s0 - s1);
+}
+
+// Constraint row -> G columns (+ history columns); returns the wave-uniform f3 = sum(G).
+// Values <= tol -> 0 (Constraints.evaluate); with clamp, G * (G > 0) (default_problem.py:93-97).
+template <bool FULL>
+__device__ __forceinline__ double constraints_row(const DProblem& p, const double* xrow,
+                                                  int lane, double* grow, double* hcols,
+                                                  bool clamp_positive) {
+  double acc3 = 0.0;
+  for (int c = lane; c < p.C; c += 64) {
+    if (p.op_code[c] == 3) continue;
+    double v = eval_op<FULL>(p, c, xrow);
+    if (v <= p.tol) v = 0.0;
+    const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
+    if (grow) grow[c] = g;
+    if (hcols) hcols[c] = g;
+    acc3 += g;
+  }
+  for (int k = 0; k < p.n_sumdiff; ++k) {
+    const int c = p.sumdiff_ops[k];
+    double v = sumdiff_wave(p, c, xrow, lane);
+    if (v <= p.tol) v = 0.0;
+    const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
+    if (lane == 0) {
+      if (grow) grow[c] = g;
+      if (hcols) hcols[c] = g;
+      acc3 += g;
+    }
+  }
+  return wave_sum(acc3);
 }
 
 // pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction.
@@ -188,7 +285,8 @@ __device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restri
 
 // Generate (mode 1) or load (mode 0) the genes of row (b, i); lane-parallel, 4 genes/lane.
 // gene_info packs kind (2 bits) | subset index << 2 | feature (or OHE group) << 17.
-__device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xrow) {
+__device__ __forceinline__ void row_genes(const RowsArgs& a, int gen, int b, int i, int lane,
+                                          double* xrow) {
   const DProblem& p = a.p;
   const int V = p.V;
   double* gout = nullptr;
@@ -214,59 +312,125 @@ __device__ void row_genes(const RowsArgs& a, int b, int i, int lane, double* xro
   const int oth = side ? par[0] : par[1];
   const double* gown = a.genes_in + ((size_t)b * a.in_rows + own) * V;
   const double* goth = a.genes_in + ((size_t)b * a.in_rows + oth) * V;
-  const Cx cx = cx_draws(rng, a.gen, m, p.n_sub, a.cx_prob);
+  const Cx cx = cx_draws(rng, gen, m, p.n_sub, a.cx_prob);
   const int nq = (V + 3) >> 2;
   const double* gl = a.s.gl + (size_t)b * V;
   const double* gu = a.s.gu + (size_t)b * V;
   for (int g0 = lane * 4; g0 < V; g0 += 256) {
     const int4 inf4 = *(const int4*)(p.gene_info + g0);  // padded to a multiple of 4
-    const u32x4 w = rng.draw((uint32_t)(i * nq + (g0 >> 2)), (uint32_t)a.gen, TAG_MUT_MASK);
+    const u32x4 w = rng.draw((uint32_t)(i * nq + (g0 >> 2)), (uint32_t)gen, TAG_MUT_MASK);
+    const int infs[4] = {inf4.x, inf4.y, inf4.z, inf4.w};
+    const uint32_t words[4] = {w.x, w.y, w.z, w.w};
     double xv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int info = j == 0 ? inf4.x : (j == 1 ? inf4.y : (j == 2 ? inf4.z : inf4.w));
-      const int kind = info & 3;
-      const int ss = kind == 0 ? 0 : 1;
+      const int info = infs[j];
+      const int ss = (info & 3) == 0 ? 0 : 1;
       const int sub = (info >> 2) & 0x7FFF;
       const bool swap = cx.on[ss] && sub >= cx.lo[ss] && sub < cx.hi[ss];
-      const double* src = swap ? goth : gown;
-      xv[j] = (g0 + j < V) ? src[g0 + j] : 0.0;
+      xv[j] = (g0 + j < V) ? (swap ? goth : gown)[g0 + j] : 0.0;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int g = g0 + j;
-      if (g >= V) break;
-      const int info = j == 0 ? inf4.x : (j == 1 ? inf4.y : (j == 2 ? inf4.z : inf4.w));
-      const uint32_t word = j == 0 ? w.x : (j == 1 ? w.y : (j == 2 ? w.z : w.w));
-      double x = xv[j];
-      if (word < a.mut_thr) {
-        const int kind = info & 3;
-        const u32x4 wu = rng.draw((uint32_t)(i * V + g), (uint32_t)a.gen, TAG_MUT_U);
-        const double u = u53(wu.x, wu.y);
-        const double xl = gl[g], xu = gu[g];
-        if (kind == 0) {
-          x = poly_mut(x, xl, xu, u, a.eta);
-        } else {
-          double y = poly_mut(x, xl - INT_WIDEN, xu + INT_WIDEN, u, a.eta);
-          y = rint(y);  // np.round: half to even
-          if (y < xl) y = xl;
-          if (y > xu) y = xu;
-          x = y;
+      if (g < V) {
+        double x = xv[j];
+        if (words[j] < a.mut_thr) {  // prob 1/V: one lane per row on average
+          const bool is_real = (infs[j] & 3) == 0;
+          const u32x4 wu = rng.draw((uint32_t)(i * V + g), (uint32_t)gen, TAG_MUT_U);
+          const double xl = gl[g], xu = gu[g];
+          const double y = poly_mut(x, is_real ? xl : xl - INT_WIDEN,
+                                    is_real ? xu : xu + INT_WIDEN, u53(wu.x, wu.y), a.eta);
+          if (is_real) {
+            x = y;
+          } else {  // IntegerFromFloatMutation: np.round (half to even), then clamp
+            double yi = rint(y);
+            if (yi < xl) yi = xl;
+            if (yi > xu) yi = xu;
+            x = yi;
+          }
         }
+        if (gout) gout[g] = x;
+        if (xrow) scatter_gene(p, xrow, infs[j], x);
       }
-      if (gout) gout[g] = x;
-      if (xrow) scatter_gene(p, xrow, info, x);
+    }
+  }
+}
+
+// Variation (mode 1) / gene load (mode 0) + decode + f2 + constraints/f3 + fp32 ML row.
+// One wave per row, 4 rows per workgroup; LDS = 4 ML rows (fp64).
+template <bool FULL>
+__global__ __launch_bounds__(256) void k_vary(int slot, int gen,
+                                              int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const DProblem& p = a.p;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= a.total) return;
+  const int b = r / a.n;
+  const int i = r - b * a.n;
+  if (!a.do_eval) {
+    row_genes(a, gen, b, i, lane, nullptr);
+    return;
+  }
+  const int D = p.D;
+  double* xrow = (double*)smem + (size_t)wave * D;
+  const double* xi = a.s.x_init + (size_t)b * D;
+  for (int f = lane; f < D; f += 64) xrow[f] = xi[f];
+  wave_sync();
+  row_genes(a, gen, b, i, lane, xrow);
+  wave_sync();
+  // fp32 ML row (scratch) + encoder MinMax distance over the mutable features
+  const int Dm = p.Dm, Dm4 = p.Dm4;
+  const double* es = a.s.enc_scale + (size_t)b * Dm;
+  const double* em = a.s.enc_min + (size_t)b * Dm;
+  const double* x0 = a.s.x0_mm + (size_t)b * Dm;
+  float* xo = a.xml + (size_t)r * Dm4;
+  const bool l2 = p.norm == 2;
+  double acc = 0.0;
+  for (int j = lane; j < Dm4; j += 64) {
+    float v = 0.f;
+    if (j < Dm) {
+      const double xf = xrow[p.mut_feat[j]];
+      v = (float)(xf * p.mlS[j] + p.mlM[j]);
+      const double d = (xf * es[j] + em[j]) - x0[j];
+      acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
+    }
+    xo[j] = v;
+  }
+  acc = l2 ? wave_sum(acc) : wave_max(acc);
+  double f2 = l2 ? sqrt(acc) : acc;
+  if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
+  double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+  double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
+  const double f3 = constraints_row<FULL>(p, xrow, lane, grow,
+                                          (hrow && a.hist_w > 3) ? hrow + 3 : nullptr, true);
+  if (lane == 0) {
+    if (a.F) {
+      const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
+      double* fr = a.F + ((size_t)b * a.out_rows + orow) * 3;
+      fr[1] = f2;
+      fr[2] = f3;
+    }
+    if (hrow) {
+      hrow[1] = f2;
+      hrow[2] = f3;
     }
   }
 }
 
 // ---------------------------------------------------------------------------------------
 // Dense layer on MFMA: out[32][N] = relu(in[32][K] . W[K][N] + bias), K % 4 == 0, N % 16 == 0.
+// Software-pipelined: U k-steps of A (LDS) and B (global/L2) fragments are loaded before
+// their 2*U MFMAs so the B-load latency is paid once per U steps.
 template <int MAXCT>
-__device__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
+__device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
                            const float* __restrict__ W, int N, const float* __restrict__ bias,
                            const float* __restrict__ bias_state, const int* row_state,
                            float* __restrict__ out, int ldo, int wave, int lane) {
+  constexpr int U = MAXCT >= 4 ? 4 : 8;
   const int nct = N >> 4;
   floatx4 acc[2][MAXCT];
 #pragma unroll
@@ -278,18 +442,29 @@ __device__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
   const int il = lane & 15;
   const float* in0 = in + il * ldi + ka;
   const float* in1 = in + (il + 16) * ldi + ka;
-#pragma unroll 4
-  for (int k0 = 0; k0 < K; k0 += 4) {
-    const float a0 = in0[k0];
-    const float a1 = in1[k0];
-    const float* wr = W + (size_t)(k0 + ka) * N + il;
+  const float* wb = W + (size_t)ka * N + il;
+  for (int k0 = 0; k0 < K; k0 += 4 * U) {
+    float a0[U], a1[U], bf[U][MAXCT];
 #pragma unroll
-    for (int c = 0; c < MAXCT; ++c) {
-      const int ct = wave + c * 4;
-      if (ct < nct) {
-        const float bf = wr[ct * 16];
-        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bf, acc[0][c], 0, 0, 0);
-        acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bf, acc[1][c], 0, 0, 0);
+    for (int u = 0; u < U; ++u) {
+      const int kk = k0 + 4 * u;
+      const bool ok = kk < K;
+      a0[u] = ok ? in0[kk] : 0.f;
+      a1[u] = ok ? in1[kk] : 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXCT; ++c) {
+        const int ct = wave + c * 4;
+        bf[u][c] = (ok && ct < nct) ? wb[(size_t)kk * N + ct * 16] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int c = 0; c < MAXCT; ++c) {
+        if (wave + c * 4 < nct) {
+          acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], bf[u][c], acc[0][c], 0, 0, 0);
+          acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], bf[u][c], acc[1][c], 0, 0, 0);
+        }
       }
     }
   }
@@ -310,7 +485,7 @@ __device__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
           } else {
             bv = bias[col];
           }
-          float v = acc[rt][c][j] + bv;
+          const float v = acc[rt][c][j] + bv;
           out[row * ldo + col] = v > 0.f ? v : 0.f;
         }
       }
@@ -318,126 +493,63 @@ __device__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
   }
 }
 
-__device__ __forceinline__ int max_hidden(const DProblem& p) {
+// Final Dense + softmax for row t (one thread), weights staged in LDS: ws[k*nout + c], wsb[c].
+__device__ __forceinline__ void last_layer_softmax(const float* in, int ldi, int K, int nout,
+                                                   const float* ws, const float* wsb, int t,
+                                                   float* prob) {
+  float mx = -__builtin_inff();
+  for (int c = 0; c < nout; ++c) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], ws[k * nout + c], s);
+    prob[c] = s + wsb[c];
+    mx = prob[c] > mx ? prob[c] : mx;
+  }
+  float den = 0.f;
+  for (int c = 0; c < nout; ++c) {
+    prob[c] = expf(prob[c] - mx);
+    den += prob[c];
+  }
+  for (int c = 0; c < nout; ++c) prob[c] = prob[c] / den;
+}
+
+__host__ __device__ inline int max_hidden(const int* dims, int n_layers) {
   int h = 16;
-  for (int l = 1; l < p.n_layers; ++l) h = p.dims[l] > h ? p.dims[l] : h;
+  for (int l = 1; l < n_layers; ++l) h = dims[l] > h ? dims[l] : h;
   return h;
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Variation (mode 1) / gene load (mode 0) + decode + f2 + constraints/f3 + fp32 ML row.
-// One wave per row, 4 rows per workgroup; LDS = 4 ML rows (fp64).
-__global__ __launch_bounds__(256) void k_vary(RowsArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const DProblem& p = a.p;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int r = blockIdx.x * 4 + wave;
-  if (r >= a.total) return;
-  const int b = r / a.n;
-  const int i = r - b * a.n;
-  double* xrow = (double*)smem + (size_t)wave * p.D;
-  if (!a.do_eval) {
-    row_genes(a, b, i, lane, nullptr);
-    return;
-  }
-  const double* xi = a.s.x_init + (size_t)b * p.D;
-#pragma unroll 4
-  for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
-  wave_sync();
-  row_genes(a, b, i, lane, xrow);
-  wave_sync();
-  // fp32 ML row (scratch) + encoder MinMax distance over the mutable features
-  const double* es = a.s.enc_scale + (size_t)b * p.Dm;
-  const double* em = a.s.enc_min + (size_t)b * p.Dm;
-  const double* x0 = a.s.x0_mm + (size_t)b * p.Dm;
-  float* xo = a.xml + (size_t)r * p.Dm4;
-  double acc = 0.0;
-#pragma unroll 2
-  for (int j = lane; j < p.Dm4; j += 64) {
-    float v = 0.f;
-    if (j < p.Dm) {
-      const double xf = xrow[p.mut_feat[j]];
-      v = (float)(xf * p.mlS[j] + p.mlM[j]);
-      const double d = (xf * es[j] + em[j]) - x0[j];
-      if (p.norm == 2)
-        acc += d * d;
-      else
-        acc = nanmax(acc, fabs(d));
-    }
-    xo[j] = v;
-  }
-  acc = p.norm == 2 ? wave_sum(acc) : wave_max(acc);
-  double f2 = p.norm == 2 ? sqrt(acc) : acc;
-  if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-  // constraint program
-  double acc3 = 0.0;
-  double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-  double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows + a.hist_row0 + i) * a.hist_w : nullptr;
-  const bool hfull = hrow && a.hist_w > 3;
-#pragma unroll 2
-  for (int c = lane; c < p.C; c += 64) {
-    if (p.op_code[c] == 3) continue;  // ABS_SUMDIFF: wave-parallel below
-    double v = eval_op(p, c, xrow);
-    if (v <= p.tol) v = 0.0;
-    const double g = v * (v > 0.0 ? 1.0 : 0.0);
-    if (grow) grow[c] = g;
-    if (hfull) hrow[3 + c] = g;
-    acc3 += g;
-  }
-  for (int k = 0; k < p.n_sumdiff; ++k) {
-    const int c = p.sumdiff_ops[k];
-    double v = sumdiff_wave(p, c, xrow, lane);
-    if (v <= p.tol) v = 0.0;
-    const double g = v * (v > 0.0 ? 1.0 : 0.0);
-    if (lane == 0) {
-      if (grow) grow[c] = g;
-      if (hfull) hrow[3 + c] = g;
-      acc3 += g;
-    }
-  }
-  acc3 = wave_sum(acc3);
-  if (lane == 0) {
-    if (a.F) {
-      const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
-      double* fr = a.F + ((size_t)b * a.out_rows + orow) * 3;
-      fr[1] = f2;
-      fr[2] = acc3;
-    }
-    if (hrow) {
-      hrow[1] = f2;
-      hrow[2] = acc3;
-    }
-  }
 }
 
 // Dense chain over 32-row tiles of the fp32 ML rows -> f1.
 template <int MAXCT>
-__global__ __launch_bounds__(EVAL_T) void k_mlp(RowsArgs a) {
+__global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int lda = p.Dm4 + 1;
-  const int hmax = max_hidden(p);
+  const int Dm4 = p.Dm4;
+  const int lda = Dm4 + 1;
+  const int nl = p.n_layers;
+  const int hmax = max_hidden(p.dims, nl);
+  const int Klast = p.dims[nl - 1];
+  const int nout = p.dims[nl];
   int* row_state = (int*)smem;  // [32]
-  const size_t head = 256;
+  float* ws = (float*)(smem + 128);
+  float* wsb = ws + Klast * nout;
+  const size_t head = mlp_head_bytes(Klast, nout);
   float* R1 = (float*)(smem + head);
-  float* R2 = (float*)(smem + head + eval_region1_bytes(p.Dm4, hmax));
+  float* R2 = (float*)(smem + head + eval_region1_bytes(Dm4, hmax));
   const int r0 = blockIdx.x * EVAL_TR;
   if (tid < EVAL_TR) row_state[tid] = (r0 + tid < a.total) ? (r0 + tid) / a.n : -1;
-  const int nq = p.Dm4 >> 2;
+  for (int q = tid; q < Klast * nout; q += EVAL_T) ws[q] = p.W[nl - 1][q];
+  if (tid < nout) wsb[tid] = p.bias[nl - 1][tid];
+  const int nq = Dm4 >> 2;
   for (int idx = tid; idx < EVAL_TR * nq; idx += EVAL_T) {
     const int t = idx / nq, q = idx - t * nq;
     const int r = r0 + t;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < a.total) v = *(const float4*)(a.xml + (size_t)r * p.Dm4 + 4 * q);
+    if (r < a.total) v = *(const float4*)(a.xml + (size_t)r * Dm4 + 4 * q);
     float* d = R1 + t * lda + 4 * q;
     d[0] = v.x;
     d[1] = v.y;
@@ -447,50 +559,33 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(RowsArgs a) {
   __syncthreads();
   const float* in = R1;
   int ldi = lda;
-  int K = p.Dm4;
+  int K = Dm4;
   float* outb = R2;
   float* other = R1;
-  for (int l = 0; l + 1 < p.n_layers; ++l) {
+  for (int l = 0; l + 1 < nl; ++l) {
     const int N = p.dims[l + 1];
-    const int ldo = N + 1;
     dense_mfma<MAXCT>(in, ldi, K, p.W[l], N, p.bias[l], l == 0 ? a.s.bias1 : nullptr, row_state,
-                      outb, ldo, wave, lane);
+                      outb, N + 1, wave, lane);
     __syncthreads();
     in = outb;
-    ldi = ldo;
+    ldi = N + 1;
     K = N;
     float* tmp = outb;
     outb = other;
     other = tmp;
   }
   if (tid < EVAL_TR) {
-    const int t = tid;
-    const int st = row_state[t];
+    const int st = row_state[tid];
     if (st >= 0) {
-      const int L = p.n_layers - 1;
-      const int nout = p.dims[L + 1];
-      const float* Wl = p.W[L];
-      const float* bl = p.bias[L];
-      float logit[8];
-      float mx = -__builtin_inff();
-      for (int c = 0; c < nout; ++c) {
-        float s = 0.f;
-        for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], Wl[(size_t)k * nout + c], s);
-        logit[c] = s + bl[c];
-        mx = logit[c] > mx ? logit[c] : mx;
-      }
-      float den = 0.f;
-      for (int c = 0; c < nout; ++c) {
-        logit[c] = expf(logit[c] - mx);
-        den += logit[c];
-      }
-      const double f1 = (double)(logit[a.s.min_class[st]] / den);
-      const int i = (r0 + t) - st * a.n;
+      float prob[8];
+      last_layer_softmax(in, ldi, K, nout, ws, wsb, tid, prob);
+      const double f1 = (double)prob[a.s.min_class[st]];
+      const int i = (r0 + tid) - st * a.n;
       if (a.F) {
         const int orow = a.out_map ? a.out_map[(size_t)st * a.n + i] : i;
         a.F[((size_t)st * a.out_rows + orow) * 3] = f1;
       }
-      if (a.hist) a.hist[((size_t)st * a.hist_rows + a.hist_row0 + i) * a.hist_w] = f1;
+      if (a.hist) a.hist[((size_t)st * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
     }
   }
 }
@@ -500,14 +595,20 @@ template <int MAXCT>
 __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int hmax = 16;
-  for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
+  const int nl = a.n_layers;
+  const int hmax = max_hidden(a.dims, nl);
+  const int Klast = a.dims[nl - 1];
+  const int nout = a.dims[nl];
   const int lda = a.D4 + 1;
-  const size_t r1 = eval_region1_bytes(a.D4, hmax);
-  float* R1 = (float*)smem;
-  float* R2 = (float*)(smem + r1);
+  float* ws = (float*)(smem + 128);
+  float* wsb = ws + Klast * nout;
+  const size_t head = mlp_head_bytes(Klast, nout);
+  float* R1 = (float*)(smem + head);
+  float* R2 = (float*)(smem + head + eval_region1_bytes(a.D4, hmax));
   const int D = a.dims[0];
   const int r0 = blockIdx.x * EVAL_TR;
+  for (int q = tid; q < Klast * nout; q += EVAL_T) ws[q] = a.W[nl - 1][q];
+  if (tid < nout) wsb[tid] = a.bias[nl - 1][tid];
   for (int idx = tid; idx < EVAL_TR * a.D4; idx += EVAL_T) {
     const int t = idx / a.D4, j = idx - t * a.D4;
     const int r = r0 + t;
@@ -518,7 +619,7 @@ __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
   int ldi = lda, K = a.D4;
   float* outb = R2;
   float* other = R1;
-  for (int l = 0; l + 1 < a.n_layers; ++l) {
+  for (int l = 0; l + 1 < nl; ++l) {
     const int N = a.dims[l + 1];
     dense_mfma<MAXCT>(in, ldi, K, a.W[l], N, a.bias[l], nullptr, nullptr, outb, N + 1, wave,
                       lane);
@@ -531,57 +632,36 @@ __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
     other = tmp;
   }
   if (tid < EVAL_TR && r0 + tid < a.n) {
-    const int t = tid;
-    const int L = a.n_layers - 1;
-    const int nout = a.dims[L + 1];
-    float logit[8];
-    float mx = -__builtin_inff();
-    for (int c = 0; c < nout; ++c) {
-      float s = 0.f;
-      for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], a.W[L][(size_t)k * nout + c], s);
-      logit[c] = s + a.bias[L][c];
-      mx = logit[c] > mx ? logit[c] : mx;
-    }
-    float den = 0.f;
-    for (int c = 0; c < nout; ++c) {
-      logit[c] = expf(logit[c] - mx);
-      den += logit[c];
-    }
-    for (int c = 0; c < nout; ++c) a.proba[(size_t)(r0 + t) * nout + c] = (double)(logit[c] / den);
+    float prob[8];
+    last_layer_softmax(in, ldi, K, nout, ws, wsb, tid, prob);
+    for (int c = 0; c < nout; ++c) a.proba[(size_t)(r0 + tid) * nout + c] = (double)prob[c];
   }
 }
 
 // Constraints only (Constraints.evaluate numpy path): one wave per ML-space row.
-__global__ __launch_bounds__(256) void k_constraints(DProblem p, int n, const double* x, double* G) {
+template <bool FULL>
+__global__ __launch_bounds__(256) void k_constraints(int slot, int n,
+                                                     const double* x, double* G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const DProblem& p = c_rows[slot].p;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = blockIdx.x * 4 + wave;
-  double* xrow = (double*)smem + (size_t)wave * p.D;
-  if (r < n)
-    for (int f = lane; f < p.D; f += 64) xrow[f] = x[(size_t)r * p.D + f];
-  __syncthreads();
   if (r >= n) return;
-  for (int c = lane; c < p.C; c += 64) {
-    if (p.op_code[c] == 3) continue;
-    double v = eval_op(p, c, xrow);
-    if (v <= p.tol) v = 0.0;
-    G[(size_t)r * p.C + c] = v;
-  }
-  for (int k = 0; k < p.n_sumdiff; ++k) {
-    const int c = p.sumdiff_ops[k];
-    double v = sumdiff_wave(p, c, xrow, lane);
-    if (v <= p.tol) v = 0.0;
-    if (lane == 0) G[(size_t)r * p.C + c] = v;
-  }
+  double* xrow = (double*)smem + (size_t)wave * p.D;
+  for (int f = lane; f < p.D; f += 64) xrow[f] = x[(size_t)r * p.D + f];
+  wave_sync();
+  constraints_row<FULL>(p, xrow, lane, G + (size_t)r * p.C, nullptr, false);
 }
 
 // Per-state constants: one workgroup per state.
-__global__ __launch_bounds__(256) void k_setup_states(DProblem p, int B, const double* x_init,
-                                                      const double* xl, const double* xu,
-                                                      const float* W1full, const float* b1,
-                                                      double* gl, double* gu, double* enc_scale,
-                                                      double* enc_min, double* x0_mm,
-                                                      float* bias1, double* genes0) {
+__global__ __launch_bounds__(256) void k_setup_states(int slot,
+                                                      const double* x_init, const double* xl,
+                                                      const double* xu, const float* W1full,
+                                                      const float* b1, double* gl, double* gu,
+                                                      double* enc_scale, double* enc_min,
+                                                      double* x0_mm, float* bias1,
+                                                      double* genes0) {
+  const DProblem& p = c_rows[slot].p;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const double* xi = x_init + (size_t)b * p.D;
@@ -652,93 +732,95 @@ static void configure_lds_once() {
   static bool done = false;
   if (done) return;
   const int lim = 160 * 1024;
-  (void)hipFuncSetAttribute((const void*)k_mlp<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_mlp<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_mlp<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_mlp<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_vary, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_predict<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_predict<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_predict<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_predict<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-  (void)hipFuncSetAttribute((const void*)k_constraints, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+  const void* fns[] = {(const void*)k_mlp<1>,          (const void*)k_mlp<2>,
+                       (const void*)k_mlp<4>,          (const void*)k_mlp<8>,
+                       (const void*)k_vary<false>,     (const void*)k_vary<true>,
+                       (const void*)k_predict<1>,      (const void*)k_predict<2>,
+                       (const void*)k_predict<4>,      (const void*)k_predict<8>,
+                       (const void*)k_constraints<false>, (const void*)k_constraints<true>};
+  for (const void* f : fns)
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
   (void)hipGetLastError();
   done = true;
 }
 
-hipError_t launch_vary(const RowsArgs& a, hipStream_t stream) {
+hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
+                       hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
   configure_lds_once();
   const size_t lds = a.do_eval ? (size_t)4 * a.p.D * sizeof(double) : 0;
-  hipLaunchKernelGGL(k_vary, dim3((a.total + 3) / 4), dim3(256), lds, stream, a);
+  const dim3 grid((a.total + 3) / 4);
+  if (a.p.full_ops)
+    hipLaunchKernelGGL(k_vary<true>, grid, dim3(256), lds, stream, slot, gen, hist_row0);
+  else
+    hipLaunchKernelGGL(k_vary<false>, grid, dim3(256), lds, stream, slot, gen, hist_row0);
   return hipGetLastError();
 }
 
-hipError_t launch_mlp(const RowsArgs& a, hipStream_t stream) {
+hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
   configure_lds_once();
-  int hmax = 16;
-  for (int l = 1; l < a.p.n_layers; ++l) hmax = a.p.dims[l] > hmax ? a.p.dims[l] : hmax;
-  const size_t lds = mlp_lds_bytes(a.p.Dm4, hmax);
-  const int grid = (a.total + EVAL_TR - 1) / EVAL_TR;
+  const int nl = a.p.n_layers;
+  const int hmax = max_hidden(a.p.dims, nl);
+  const size_t lds = mlp_lds_bytes(a.p.Dm4, hmax, a.p.dims[nl - 1], a.p.dims[nl]);
+  const dim3 grid((a.total + EVAL_TR - 1) / EVAL_TR);
   const int nct = hmax / 16;
   if (nct <= 4)
-    hipLaunchKernelGGL(k_mlp<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<1>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
   else if (nct <= 8)
-    hipLaunchKernelGGL(k_mlp<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<2>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
   else if (nct <= 16)
-    hipLaunchKernelGGL(k_mlp<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<4>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
   else
-    hipLaunchKernelGGL(k_mlp<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_mlp<8>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
-hipError_t launch_rows(const RowsArgs& a, hipStream_t stream) {
-  hipError_t e = launch_vary(a, stream);
+hipError_t launch_rows(const RowsArgs& a, int slot, int gen, int hist_row0,
+                       hipStream_t stream) {
+  hipError_t e = launch_vary(a, slot, gen, hist_row0, stream);
   if (e != hipSuccess || !a.do_eval) return e;
-  return launch_mlp(a, stream);
+  return launch_mlp(a, slot, hist_row0, stream);
 }
 
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream) {
   if (a.n <= 0) return hipSuccess;
   configure_lds_once();
-  int hmax = 16;
-  for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
-  const size_t lds = eval_region1_bytes(a.D4, hmax) + (size_t)EVAL_TR * (hmax + 1) * 4;
-  const int grid = (a.n + EVAL_TR - 1) / EVAL_TR;
+  const int nl = a.n_layers;
+  const int hmax = max_hidden(a.dims, nl);
+  const size_t lds = mlp_lds_bytes(a.D4, hmax, a.dims[nl - 1], a.dims[nl]);
+  const dim3 grid((a.n + EVAL_TR - 1) / EVAL_TR);
   const int nct = hmax / 16;
   if (nct <= 4)
-    hipLaunchKernelGGL(k_predict<1>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_predict<1>, grid, dim3(EVAL_T), lds, stream, a);
   else if (nct <= 8)
-    hipLaunchKernelGGL(k_predict<2>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_predict<2>, grid, dim3(EVAL_T), lds, stream, a);
   else if (nct <= 16)
-    hipLaunchKernelGGL(k_predict<4>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_predict<4>, grid, dim3(EVAL_T), lds, stream, a);
   else
-    hipLaunchKernelGGL(k_predict<8>, dim3(grid), dim3(EVAL_T), lds, stream, a);
+    hipLaunchKernelGGL(k_predict<8>, grid, dim3(EVAL_T), lds, stream, a);
   return hipGetLastError();
 }
 
-hipError_t launch_constraints(const DProblem& p, int n, const double* x, double* G,
-                              hipStream_t stream) {
+hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double* x,
+                              double* G, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   configure_lds_once();
-  hipLaunchKernelGGL(k_constraints, dim3((n + 3) / 4), dim3(256), (size_t)4 * p.D * 8, stream, p,
-                     n, x, G);
+  const size_t lds = (size_t)4 * hp.D * sizeof(double);
+  const dim3 grid((n + 3) / 4);
+  if (hp.full_ops)
+    hipLaunchKernelGGL(k_constraints<true>, grid, dim3(256), lds, stream, slot, n, x, G);
+  else
+    hipLaunchKernelGGL(k_constraints<false>, grid, dim3(256), lds, stream, slot, n, x, G);
   return hipGetLastError();
 }
 
-hipError_t launch_variation(const RowsArgs& a, hipStream_t stream) {
-  RowsArgs v = a;
-  v.do_eval = 0;
-  return launch_vary(v, stream);
-}
-
-hipError_t launch_setup_states(const DProblem& p, int B, const double* x_init, const double* xl,
+hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,
                                const double* xu, const float* W1full, const float* b1, double* gl,
                                double* gu, double* enc_scale, double* enc_min, double* x0_mm,
                                float* bias1, double* genes0, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_setup_states, dim3(B), dim3(256), 0, stream, p, B, x_init, xl, xu, W1full,
+  hipLaunchKernelGGL(k_setup_states, dim3(B), dim3(256), 0, stream, slot, x_init, xl, xu, W1full,
                      b1, gl, gu, enc_scale, enc_min, x0_mm, bias1, genes0);
   return hipGetLastError();
 }

@@ -28,7 +28,7 @@ struct SurvLds {
   double* ref;      // [R*3]
   double* U;        // [(R+3)*3] normalised reference directions
   double* dist;     // [N]
-  double* red;      // [4*16] reduction scratch
+  double* red;      // [waves*16] reduction scratch
   double* scal;     // [32] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9)
   unsigned long long* dom;     // [N*NW]
   unsigned long long* ranked;  // [NW]
@@ -50,80 +50,79 @@ struct SurvLds {
   int* cand;        // [R+3]
   int* ckey;        // [R+3]
   int* iscal;       // [16]
-  int* selkey;      // [n_perm_slots]
+  unsigned long long* sortk;  // [pow2 >= max(N, n_perm_slots)] bitonic sort keys
   int* perm;        // [n_perm_slots]
   unsigned long long* dmin;  // [R+3]
-  int* lhist;       // [2N+2] picks per level -> prefix
   int* lround;      // [2N+2] round index of each level
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-__host__ __device__ inline size_t surv_layout(int N, int R, int Pperm, SurvLds* L, unsigned char* base) {
-  const int NW = (N + 63) / 64;
-  const int RN = R + 3;
-  size_t off = 0;
-  auto take = [&](size_t bytes) {
-    size_t o = off;
-    off = align16(off + bytes);
-    return o;
-  };
-  const size_t oF = take((size_t)N * 3 * 8), oRef = take((size_t)R * 3 * 8),
-               oU = take((size_t)RN * 3 * 8), oDist = take((size_t)N * 8), oRed = take(64 * 8),
-               oScal = take(32 * 8), oDom = take((size_t)N * NW * 8), oRk = take(NW * 8),
-               oCur = take(NW * 8), oI = take(N * 4), oPos = take(N * 4), oFo = take(N * 4),
-               oSlot = take(N * 4), oNi = take(N * 4), oMe = take(N * 4), oKey = take(N * 4),
-               oSurv = take(N * 4), oSel = take(N * 4), oFs = take((N + 2) * 4),
-               oCnt = take(RN * 4), oRem = take(RN * 4), oCo = take((RN + 1) * 4),
-               oCsr = take(N * 4), oCand = take(RN * 4), oCk = take(RN * 4), oIs = take(16 * 4),
-               oSk = take((size_t)Pperm * 4), oPerm = take((size_t)Pperm * 4),
-               oDmin = take((size_t)RN * 8), oLh = take((size_t)(2 * N + 2) * 4),
-               oLr = take((size_t)(2 * N + 2) * 4);
-  if (L) {
-    L->F = (double*)(base + oF);
-    L->ref = (double*)(base + oRef);
-    L->U = (double*)(base + oU);
-    L->dist = (double*)(base + oDist);
-    L->red = (double*)(base + oRed);
-    L->scal = (double*)(base + oScal);
-    L->dom = (unsigned long long*)(base + oDom);
-    L->ranked = (unsigned long long*)(base + oRk);
-    L->cur = (unsigned long long*)(base + oCur);
-    L->I = (int*)(base + oI);
-    L->pos = (int*)(base + oPos);
-    L->front_of = (int*)(base + oFo);
-    L->slot = (int*)(base + oSlot);
-    L->niche = (int*)(base + oNi);
-    L->memb = (int*)(base + oMe);
-    L->key = (int*)(base + oKey);
-    L->surv = (int*)(base + oSurv);
-    L->sel = (int*)(base + oSel);
-    L->fstart = (int*)(base + oFs);
-    L->count = (int*)(base + oCnt);
-    L->remain = (int*)(base + oRem);
-    L->csr_off = (int*)(base + oCo);
-    L->csr = (int*)(base + oCsr);
-    L->cand = (int*)(base + oCand);
-    L->ckey = (int*)(base + oCk);
-    L->iscal = (int*)(base + oIs);
-    L->selkey = (int*)(base + oSk);
-    L->perm = (int*)(base + oPerm);
-    L->dmin = (unsigned long long*)(base + oDmin);
-    L->lhist = (int*)(base + oLh);
-    L->lround = (int*)(base + oLr);
-  }
-  return off;
+__host__ __device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// Byte offsets of the survival workspace inside the dynamic LDS block.
+struct SurvOff {
+  unsigned F, ref, U, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
+      key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm, dmin,
+      lround, total;
+};
+
+__host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
+  const unsigned NW = (N + 63) / 64;
+  const unsigned RN = R + 3;
+  SurvOff o;
+  unsigned off = 0;
+#define TAKE(field, bytes)        \
+  o.field = off;                  \
+  off = (unsigned)align16(off + (size_t)(bytes));
+  TAKE(F, (size_t)N * 3 * 8)
+  TAKE(ref, (size_t)R * 3 * 8)
+  TAKE(U, (size_t)RN * 3 * 8)
+  TAKE(dist, (size_t)N * 8)
+  TAKE(red, (SURV_T / 64) * 16 * 8)
+  TAKE(scal, 32 * 8)
+  TAKE(dom, (size_t)N * NW * 8)
+  TAKE(ranked, NW * 8)
+  TAKE(cur, NW * 8)
+  TAKE(I, N * 4)
+  TAKE(pos, N * 4)
+  TAKE(front_of, N * 4)
+  TAKE(slot, N * 4)
+  TAKE(niche, N * 4)
+  TAKE(memb, N * 4)
+  TAKE(key, N * 4)
+  TAKE(surv, N * 4)
+  TAKE(sel, N * 4)
+  TAKE(fstart, (N + 2) * 4)
+  TAKE(count, RN * 4)
+  TAKE(remain, RN * 4)
+  TAKE(csr_off, (RN + 1) * 4)
+  TAKE(csr, N * 4)
+  TAKE(cand, RN * 4)
+  TAKE(ckey, RN * 4)
+  TAKE(iscal, 16 * 4)
+  TAKE(sortk, (size_t)pow2_at_least(N > Pperm ? N : Pperm) * 8)
+  TAKE(perm, (size_t)Pperm * 4)
+  TAKE(dmin, (size_t)RN * 8)
+  TAKE(lround, (size_t)(2 * N + 2) * 4)
+#undef TAKE
+  o.total = off;
+  return o;
 }
 
 __device__ __forceinline__ double min_prop(double a, double b) {  // np.min (NaN propagates)
-  if (a != a) return a;
-  if (b != b) return b;
-  return b < a ? b : a;
+  double r = b < a ? b : a;
+  r = b != b ? b : r;
+  return a != a ? a : r;
 }
 __device__ __forceinline__ double max_prop(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  return b > a ? b : a;
+  double r = b > a ? b : a;
+  r = b != b ? b : r;
+  return a != a ? a : r;
 }
 
 // np.argmin order: first NaN, else smallest value, ties -> smallest index
@@ -142,7 +141,7 @@ __device__ __forceinline__ bool dominates(const double* a, const double* b) {
 // Ordered stream compaction of the indices i in [0, n) with pred(i) into out[base..].
 // Returns the count (uniform).  Uses red scratch as int[4+1].
 template <class Pred>
-__device__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
+__device__ __forceinline__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int total = 0;
   for (int b0 = 0; b0 < n; b0 += SURV_T) {
@@ -162,6 +161,35 @@ __device__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
     __syncthreads();
   }
   return total;
+}
+
+// Exclusive prefix sum of v[0, n) in place (LDS); returns the total (uniform).
+__device__ __forceinline__ int block_scan_excl(int* v, int n, int* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int carry = 0;
+  for (int b0 = 0; b0 < n; b0 += SURV_T) {
+    const int i = b0 + tid;
+    const int x = i < n ? v[i] : 0;
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SURV_T / 64; ++w) {
+      const int sw = wsum[w];
+      if (w < wave) woff += sw;
+      tot += sw;
+    }
+    if (i < n) v[i] = carry + woff + incl - x;
+    carry += tot;
+    __syncthreads();
+  }
+  return carry;
 }
 
 __device__ __forceinline__ double wred_min(double v) {
@@ -203,27 +231,54 @@ __device__ bool lu_solve3(double A[3][3], double x[3]) {
   return true;
 }
 
+// Ascending bitonic sort of k[0, n2) (n2 a power of two; callers pad with ~0).  Keys are
+// unique composites (order fields << ... | index), so the order is total and deterministic.
+__device__ __forceinline__ void block_sort_u64(unsigned long long* k, int n2) {
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < n2; i += SURV_T) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const unsigned long long x = k[i], y = k[j];
+          const bool up = (i & size) == 0;
+          if ((x > y) == up) {
+            k[i] = y;
+            k[j] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Tournament selection for the next generation (oracle tournament_parents).
-__device__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
-                           const int* map_slot, int* out, int* selkey, int* perm) {
+__device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
+                           const int* map_slot, int* out, unsigned long long* sortk,
+                           int* perm) {
   const int tid = threadIdx.x;
   const int n_m = (O_next + 1) / 2;
   const int n_random = n_m * 4;
   const int n_perms = (n_random + P - 1) / P;
+  const int n = n_perms * P;
+  const int n2 = pow2_at_least(n);
   const Rng rng(seed, sk);
-  for (int idx = tid; idx < n_perms * P; idx += SURV_T)
-    selkey[idx] = (int)rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
-  __syncthreads();
-  for (int idx = tid; idx < n_perms * P; idx += SURV_T) {
-    const int q = idx / P, i = idx - q * P;
-    const unsigned ki = (unsigned)selkey[idx];
-    int r = 0;
-    for (int j = 0; j < P; ++j) {
-      const unsigned kj = (unsigned)selkey[q * P + j];
-      r += (kj < ki) || (kj == ki && j < i);
+  int ib = 1;  // bits of the index field
+  while ((1 << ib) < P) ++ib;
+  const unsigned long long imask = (1ull << ib) - 1ull;
+  // permutation q = argsort of its P keys (ties by index): sort (q, key, i) composites
+  for (int idx = tid; idx < n2; idx += SURV_T) {
+    unsigned long long v = ~0ull;
+    if (idx < n) {
+      const int q = idx / P, i = idx - q * P;
+      const unsigned key = rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
+      v = ((unsigned long long)q << (32 + ib)) | ((unsigned long long)key << ib) | (unsigned)i;
     }
-    perm[q * P + r] = i;
+    sortk[idx] = v;
   }
+  __syncthreads();
+  block_sort_u64(sortk, n2);
+  for (int idx = tid; idx < n; idx += SURV_T) perm[idx] = (int)(sortk[idx] & imask);
   __syncthreads();
   for (int t = tid; t < 2 * n_m; t += SURV_T) {
     const int a = perm[2 * t], b = perm[2 * t + 1];
@@ -243,8 +298,38 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   const int NW = (N + 63) / 64;
   const int n_m_next = a.parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = a.parents_out ? ((n_m_next * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
+  const SurvOff o = surv_offsets(N, R, pslots);
   SurvLds L;
-  surv_layout(N, R, pslots, &L, smem);
+  L.F = (double*)(smem + o.F);
+  L.ref = (double*)(smem + o.ref);
+  L.U = (double*)(smem + o.U);
+  L.dist = (double*)(smem + o.dist);
+  L.red = (double*)(smem + o.red);
+  L.scal = (double*)(smem + o.scal);
+  L.dom = (unsigned long long*)(smem + o.dom);
+  L.ranked = (unsigned long long*)(smem + o.ranked);
+  L.cur = (unsigned long long*)(smem + o.cur);
+  L.I = (int*)(smem + o.I);
+  L.pos = (int*)(smem + o.pos);
+  L.front_of = (int*)(smem + o.front_of);
+  L.slot = (int*)(smem + o.slot);
+  L.niche = (int*)(smem + o.niche);
+  L.memb = (int*)(smem + o.memb);
+  L.key = (int*)(smem + o.key);
+  L.surv = (int*)(smem + o.surv);
+  L.sel = (int*)(smem + o.sel);
+  L.fstart = (int*)(smem + o.fstart);
+  L.count = (int*)(smem + o.count);
+  L.remain = (int*)(smem + o.remain);
+  L.csr_off = (int*)(smem + o.csr_off);
+  L.csr = (int*)(smem + o.csr);
+  L.cand = (int*)(smem + o.cand);
+  L.ckey = (int*)(smem + o.ckey);
+  L.iscal = (int*)(smem + o.iscal);
+  L.sortk = (unsigned long long*)(smem + o.sortk);
+  L.perm = (int*)(smem + o.perm);
+  L.dmin = (unsigned long long*)(smem + o.dmin);
+  L.lround = (int*)(smem + o.lround);
   double* ideal = L.scal;
   double* worst = L.scal + 3;
   double* wpop = L.scal + 6;
@@ -252,6 +337,9 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   double* nadir = L.scal + 12;
   double* ext = L.scal + 15;  // 9
   const bool slot_mode = a.pop_slot != nullptr;
+#define PHASE(k) \
+  if (a.phase && tid == 0) a.phase[(size_t)b * 16 + (k)] = clock64();
+  PHASE(0)
 
   // ---- load merged F, ref points
   for (int m = tid; m < N; m += SURV_T) {
@@ -276,6 +364,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     L.cur[q] = 0ull;
   }
   __syncthreads();
+  PHASE(1)
 
   // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population
   {
@@ -324,18 +413,35 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       wpop[k] = vwp;
     }
   }
+  PHASE(11)
 
-  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j
-  for (int j = wave; j < N; j += SURV_T / 64) {
-    const double fj[3] = {L.F[j * 3], L.F[j * 3 + 1], L.F[j * 3 + 2]};
-    for (int q = 0; q < NW; ++q) {
+  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Lane l keeps the rows
+  // i = 64q + l in registers (NaN rows dominate nothing); a wave sweeps j.
+  {
+    constexpr int NWMAX = SURV_NMAX / 64;
+    double fi[NWMAX][3];
+#pragma unroll
+    for (int q = 0; q < NWMAX; ++q) {
       const int i = q * 64 + lane;
-      const bool d = i < N && dominates(&L.F[i * 3], fj);
-      const unsigned long long msk = __ballot(d);
-      if (lane == 0) L.dom[(size_t)j * NW + q] = msk;
+      const bool ok = q < NW && i < N;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) fi[q][k] = ok ? L.F[i * 3 + k] : __builtin_nan("");
+    }
+    for (int j = wave; j < N; j += SURV_T / 64) {
+      const double fj[3] = {L.F[j * 3], L.F[j * 3 + 1], L.F[j * 3 + 2]};
+      unsigned long long mine = 0ull;
+#pragma unroll
+      for (int q = 0; q < NWMAX; ++q) {
+        if (q < NW) {
+          const unsigned long long msk = __ballot(dominates(fi[q], fj));
+          if (lane == q) mine = msk;
+        }
+      }
+      if (lane < NW) L.dom[(size_t)j * NW + lane] = mine;
     }
   }
   __syncthreads();
+  PHASE(2)
 
   // ---- fast non-dominated sort (discovery order), stop once >= n_survive ranked
   int* wsum = L.iscal;  // [0..3]
@@ -406,6 +512,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     __syncthreads();
   }
   const int n_ranked = cum;
+  PHASE(3)
 
   // ---- extreme points (ASF over prev extremes + front 0 + ref points), worst of front
   {
@@ -529,6 +636,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     }
     __syncthreads();
   }
+  PHASE(4)
 
   // ---- aspiration reference directions (normalised), R points + 3 extreme axes
   {
@@ -562,8 +670,10 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
       for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
     }
+    if (tid == 0) L.iscal[15] = 0;
     __syncthreads();
   }
+  PHASE(5)
 
   // ---- association of the ranked individuals (I order) to the nearest direction
   {
@@ -576,37 +686,59 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      // argmin over squared distances (first index on exact ties, like np.argmin).  Two
+      // DIFFERENT squared distances can share a sqrt: flag when a distance differs from the
+      // running best by at most 1e-15 relative (or is NaN); the exact np.argmin over the
+      // sqrt'ed values below then decides.  Branchless, 4 directions per step.
       double best = __builtin_inf();
       int bj = 0;
       bool flag = false;
+      const double c = 1.0 + 1e-15;
+      auto d2_of = [&](int j) {
+        const double* u = &L.U[j * 3];
+        const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+        const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+        return (e0 * e0 + e1 * e1) + e2 * e2;
+      };
+      auto take = [&](double d2, int j) {
+        flag = flag | (d2 != d2) | ((d2 != best) & (d2 <= best * c) & (best <= d2 * c));
+        const bool lt = d2 < best;
+        best = lt ? d2 : best;
+        bj = lt ? j : bj;
+      };
+      int j0 = 0;
+      for (; j0 + 4 <= RN; j0 += 4) {
+        const double d0 = d2_of(j0), d1 = d2_of(j0 + 1), d2 = d2_of(j0 + 2), d3 = d2_of(j0 + 3);
+        take(d0, j0);
+        take(d1, j0 + 1);
+        take(d2, j0 + 2);
+        take(d3, j0 + 3);
+      }
+      for (; j0 < RN; ++j0) take(d2_of(j0), j0);
+      L.niche[p] = bj;
+      L.dist[p] = sqrt(best);
+      if (flag) L.key[atomicAdd(&L.iscal[15], 1)] = p;
+    }
+    __syncthreads();
+    PHASE(10)
+    // exact np.argmin over sqrt'ed distances for the flagged individuals
+    const int n_flag = L.iscal[15];
+    if (a.phase && tid == 0) a.phase[(size_t)b * 16 + 12] = n_flag;
+    for (int t = tid; t < n_flag; t += SURV_T) {
+      const int p = L.key[t];
+      const int m = L.I[p];
+      double Nn[3];
+      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      double bd = __builtin_inf();
+      int bj = 0;
       for (int j = 0; j < RN; ++j) {
         const double* u = &L.U[j * 3];
         const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
         const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
-        const double d2 = (e0 * e0 + e1 * e1) + e2 * e2;
-        if (d2 != d2) {
-          flag = true;
-        } else if (d2 < best) {
-          if (best <= d2 * (1.0 + 1e-15)) flag = true;
-          best = d2;
+        const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+        if (arg_better(dd, j, bd, bj)) {
+          bd = dd;
           bj = j;
-        } else if (d2 <= best * (1.0 + 1e-15)) {
-          flag = true;
-        }
-      }
-      double bd = sqrt(best);
-      if (flag) {  // exact np.argmin over sqrt'ed distances
-        bd = __builtin_inf();
-        bj = 0;
-        for (int j = 0; j < RN; ++j) {
-          const double* u = &L.U[j * 3];
-          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
-          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
-          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
-          if (arg_better(dd, j, bd, bj)) {
-            bd = dd;
-            bj = j;
-          }
         }
       }
       L.niche[p] = bj;
@@ -614,6 +746,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     }
     __syncthreads();
   }
+  PHASE(6)
 
   // ---- survivor selection: fronts until the last + niching on the last front
   int n_out;
@@ -629,10 +762,8 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     const int n_rem = nf == 1 ? a.n_survive : a.n_survive - fs;
     const int until = nf == 1 ? 0 : fs;
     const Rng rng(a.seed, a.stream_key);
-    int* mkey = L.key;
     int* grank = L.memb;
     int* lev = L.csr;
-    int* K = L.pos;
     int* cnt = L.count;
     int* mcnt = L.remain;
     int* start = L.csr_off;
@@ -646,35 +777,32 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       L.dmin[n] = ~0ull;
       bestkr[n] = INT_MAX;
     }
-    for (int l = tid; l <= nlev; l += SURV_T) L.lhist[l] = 0;
-    __syncthreads();
+    for (int l = tid; l < nlev; l += SURV_T) L.lround[l] = 0;
+    const int n2 = pow2_at_least(Lc);
+    unsigned long long* sk = L.sortk;
     for (int p = tid; p < until; p += SURV_T) atomicAdd(&cnt[L.niche[p]], 1);
-    for (int p = tid; p < Lc; p += SURV_T) {
-      atomicAdd(&mcnt[nich[p]], 1);
-      mkey[p] = (int)rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
+    // member order inside each niche: ascending (niche, member key, position)
+    for (int p = tid; p < n2; p += SURV_T) {
+      unsigned long long v = ~0ull;
+      if (p < Lc) {
+        const unsigned key = rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
+        atomicAdd(&mcnt[nich[p]], 1);
+        v = ((unsigned long long)nich[p] << 41) | ((unsigned long long)key << 9) | (unsigned)p;
+      }
+      sk[p] = v;
     }
     __syncthreads();
-    for (int p = tid; p < Lc; p += SURV_T) {
+    block_sort_u64(sk, n2);
+    for (int r = tid; r < Lc; r += SURV_T) {
+      const int p = (int)(sk[r] & 511ull);
       const int np_ = nich[p];
-      const unsigned kp = (unsigned)mkey[p];
-      int r = 0;
-      for (int q = 0; q < Lc; ++q) {
-        const int nq = nich[q];
-        const unsigned kq = (unsigned)mkey[q];
-        r += (nq < np_) || (nq == np_ && (kq < kp || (kq == kp && q < p)));
-      }
       grank[p] = r;
       if (cnt[np_] == 0)
         atomicMin(&L.dmin[np_], (unsigned long long)__double_as_longlong(dst[p]));
     }
-    if (tid == 0) {
-      int acc = 0;
-      for (int n = 0; n < RN; ++n) {
-        start[n] = acc;
-        acc += mcnt[n];
-      }
-    }
+    for (int n = tid; n < RN; n += SURV_T) start[n] = mcnt[n];
     __syncthreads();
+    block_scan_excl(start, RN, wsum);
     for (int p = tid; p < Lc; p += SURV_T) {
       const int np_ = nich[p];
       if (cnt[np_] == 0 && (unsigned long long)__double_as_longlong(dst[p]) == L.dmin[np_])
@@ -688,44 +816,26 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       if (cnt[np_] == 0) j = kr == bestkr[np_] ? 0 : kr + (kr < bestkr[np_] ? 1 : 0);
       const int l = cnt[np_] + j;
       lev[p] = l;
-      atomicAdd(&L.lhist[l], 1);
+      L.lround[l] = 1;  // level is non-empty
     }
     __syncthreads();
-    if (tid == 0) {
-      int acc = 0, rnd = 0;
-      for (int l = 0; l < nlev; ++l) {
-        const int h = L.lhist[l];
-        L.lhist[l] = acc;
-        L.lround[l] = rnd;
-        if (h) {
-          acc += h;
-          ++rnd;
-        }
+    block_scan_excl(L.lround, nlev, wsum);  // rounds before each level
+    // output order: ascending (level, round key of the niche, niche); a niche picks at most
+    // once per level, so the sorted index is the pick's position among the remaining slots
+    for (int p = tid; p < n2; p += SURV_T) {
+      unsigned long long v = ~0ull;
+      if (p < Lc) {
+        const int l = lev[p];
+        const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
+                                     TAG_NICHE_PERM).x;
+        v = ((unsigned long long)l << 51) | ((unsigned long long)kr << 19) |
+            ((unsigned long long)nich[p] << 9) | (unsigned)p;
       }
-      L.lhist[nlev] = acc;
+      sk[p] = v;
     }
     __syncthreads();
-    for (int p = tid; p < Lc; p += SURV_T) {
-      const int l = lev[p];
-      if (L.lhist[l] < n_rem)
-        K[p] = (int)rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
-                             TAG_NICHE_PERM).x;
-    }
-    __syncthreads();
-    for (int p = tid; p < Lc; p += SURV_T) {
-      const int l = lev[p];
-      const int base = L.lhist[l];
-      if (base >= n_rem) continue;
-      const unsigned kp = (unsigned)K[p];
-      const int np_ = nich[p];
-      int r = 0;
-      for (int q = 0; q < Lc; ++q) {
-        if (lev[q] != l) continue;
-        const unsigned kq = (unsigned)K[q];
-        r += kq < kp || (kq == kp && nich[q] < np_);
-      }
-      if (base + r < n_rem) L.surv[until + base + r] = fs + p;
-    }
+    block_sort_u64(sk, n2);
+    for (int r = tid; r < n_rem; r += SURV_T) L.surv[until + r] = fs + (int)(sk[r] & 511ull);
     for (int p = tid; p < until; p += SURV_T) L.surv[p] = p;
     n_out = a.n_survive;
   } else {
@@ -733,6 +843,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     n_out = n_ranked;
   }
   __syncthreads();
+  PHASE(7)
 
   // ---- outputs
   for (int k = tid; k < N; k += SURV_T) L.memb[k] = 0;  // selected flags by merged index
@@ -774,11 +885,15 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     for (int k = tid; k < nfree; k += SURV_T)
       a.free_slot[(size_t)b * a.O + k] = L.slot[L.key[k]];
   }
+  __syncthreads();
+  PHASE(8)
   if (a.parents_out) {
-    __syncthreads();
     tournament(a.n_survive, a.O_next, a.seed, a.stream_key, a.sel_gen, slot_mode ? L.sel : nullptr,
-               a.parents_out + (size_t)b * n_m_next * 2, L.selkey, L.perm);
+               a.parents_out + (size_t)b * n_m_next * 2, L.sortk, L.perm);
   }
+  __syncthreads();
+  PHASE(9)
+#undef PHASE
 }
 
 __global__ __launch_bounds__(SURV_T) void k_select(int P, int O, uint64_t seed, uint32_t sk,
@@ -787,8 +902,8 @@ __global__ __launch_bounds__(SURV_T) void k_select(int P, int O, uint64_t seed, 
   const int b = blockIdx.x;
   const int n_m = (O + 1) / 2;
   const int slots = ((n_m * 4 + P - 1) / P) * P;
-  int* key = (int*)smem;
-  int* perm = key + slots;
+  unsigned long long* key = (unsigned long long*)smem;
+  int* perm = (int*)(key + pow2_at_least(slots));
   tournament(P, O, seed, sk, gen, pop_slot ? pop_slot + (size_t)b * P : nullptr,
              parents + (size_t)b * n_m * 2, key, perm);
 }
@@ -825,7 +940,7 @@ __global__ void k_gather_pop(int B, int P, int V, int S, const int* pop_slot, co
   }
 }
 
-size_t surv_lds_bytes(int N, int R, int Pperm) { return surv_layout(N, R, Pperm, nullptr, nullptr); }
+size_t surv_lds_bytes(int N, int R, int Pperm) { return surv_offsets(N, R, Pperm).total; }
 
 hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
@@ -848,7 +963,8 @@ hipError_t launch_select(int B, int P, int O, uint64_t seed, uint32_t sk, int ge
   if (B <= 0) return hipSuccess;
   const int n_m = (O + 1) / 2;
   const int slots = ((n_m * 4 + P - 1) / P) * P;
-  hipLaunchKernelGGL(k_select, dim3(B), dim3(SURV_T), (size_t)slots * 8, stream, P, O, seed, sk,
+  const size_t lds = (size_t)pow2_at_least(slots) * 8 + (size_t)slots * 4;
+  hipLaunchKernelGGL(k_select, dim3(B), dim3(SURV_T), lds, stream, P, O, seed, sk,
                      gen, pop_slot, parents);
   return hipGetLastError();
 }

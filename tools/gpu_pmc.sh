@@ -11,7 +11,7 @@ while read -r group; do
      --output-format csv -- python3 bench.py $ARGS > gpurun_out/pmc/p$i.log 2>&1
   rc=$?; echo "pass $i ($group) rc=$rc"
   case $rc in 124|134|137|139) echo stop; exit $rc;; esac
-done <<< "${GROUPS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU
+done <<< "${PMC_GROUPS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU
 FETCH_SIZE
 WRITE_SIZE
 SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE}"
