@@ -184,19 +184,41 @@ def main():
     kt = eng.kernel_times()
     eng.set_profiling(False)
     ng = max(kt["generations"], 1)
-    vary_ms = kt["vary_ms"] / ng
+    gen_ms = kt["gen_ms"] / ng
+    cons_ms = kt["cons_ms"] / ng
     mlp_ms = kt["mlp_ms"] / ng
     surv_ms = kt["survive_ms"] / ng
     rows = B * O
-    Dm4 = (int(eng.prog.mut_feats.shape[0]) + 3) // 4 * 4
-    # k_vary algorithmic bytes per offspring row (SURVEY.md §8d form): parent genes read +
-    # child genes written (2*V*8) + f2/f3 (16) + the fp32 ML row handed to k_mlp (Dm4*4)
-    vary_bytes = 2 * V * 8 + 16 + Dm4 * 4
-    vary_gbs = vary_bytes * rows / (vary_ms * 1e-3) / 1e9
-    dims = [int(eng.prog.mut_feats.shape[0])] + list(eng_dims(eng))[1:]
+    Dm = int(eng.prog.mut_feats.shape[0])
+    Dm4 = (Dm + 3) // 4 * 4
+    # algorithmic bytes per offspring row (SURVEY.md §8d form):
+    #   k_gen : parent genes read + child genes written (2*V*8) + fp32 ML row (Dm4*4) + f2 (8)
+    #   k_cons: child genes read (V*8) + f3 (8)
+    #   k_survive: merged F read (N*3*8) + survivor/free slots + parents (4*(P+O+O)) per state
+    gen_bytes = 2 * V * 8 + Dm4 * 4 + 8
+    cons_bytes = V * 8 + 8
+    surv_bytes_state = (P + O) * 3 * 8 + 4 * (P + 2 * O)
+    dims = [Dm] + list(eng_dims(eng))[1:]
     mlp_flops = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
-    mlp_tfs = mlp_flops * rows / (mlp_ms * 1e-3) / 1e12
-    dom = max(("k_vary", vary_ms), ("k_mlp", mlp_ms), ("k_survive", surv_ms), key=lambda t: t[1])
+
+    def hbm(name, bytes_launch, ms):
+        gbs = bytes_launch / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": None, "kernel": name,
+                "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": ms}
+
+    kernels = {
+        "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows, gen_ms),
+        "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms),
+        "k_mlp": {"bound": "mfma", "achieved": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12,
+                  "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                  "frac": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
+                  "traffic": None, "kernel": "k_mlp (fp32 MFMA Dense chain)",
+                  "algorithmic_flops_per_launch": mlp_flops * rows, "avg_launch_ms": mlp_ms},
+        "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
+                         surv_bytes_state * B, surv_ms),
+    }
+    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
 
     result = {
         "metric": "candidate fitness evals/sec (whole node) + attack wall-clock per 1k states",
@@ -219,17 +241,10 @@ def main():
                    "parallelism": f"states x{world} (independent per-rank shards)"},
         "attack_wall_clock_per_1k_states_s": elapsed / args.steps / (world * B) * 1000.0,
         "load_s": load_s,
-        "roofline": {"bound": "hbm", "achieved": vary_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": vary_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_vary (variation + decode + constraints + distance)",
-                     "algorithmic_bytes_per_launch": vary_bytes * rows,
-                     "avg_launch_ms": vary_ms},
-        "mlp_roofline": {"bound": "mfma", "achieved": mlp_tfs, "peak": MFMA_F32_PEAK_TFS,
-                         "unit": "TFLOP/s", "frac": mlp_tfs / MFMA_F32_PEAK_TFS,
-                         "kernel": "k_mlp (fp32 MFMA Dense chain)",
-                         "algorithmic_flops_per_launch": mlp_flops * rows, "avg_launch_ms": mlp_ms},
-        "kernels_avg_ms_per_generation": {"k_vary": vary_ms, "k_mlp": mlp_ms, "k_survive": surv_ms,
-                                          "dominant": dom[0]},
+        "roofline": kernels[dom],
+        "kernels": kernels,
+        "kernels_avg_ms_per_generation": {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms,
+                                          "k_survive": surv_ms, "dominant": dom},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline(w, 1, args.cpu_gens)

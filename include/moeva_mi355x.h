@@ -163,6 +163,10 @@ int mv_attack_history(mv_engine* e, double* hist, void* stream);
 int mv_set_profiling(mv_engine* e, int32_t enabled);
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations);
+/* Same events, split by kernel: ms[0] k_gen (variation + ML row + f2), ms[1] k_cons
+ * (constraints + f3), ms[2] k_mlp (classifier, f1), ms[3] k_survive (survival + next
+ * tournament), summed over the profiled generations. */
+int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -100,7 +101,7 @@ struct mv_engine {
   }
   // profiling
   bool profiling = false;
-  std::vector<hipEvent_t> ev_var, ev_mlp, ev_surv;
+  std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
   int n_var_rec = 0, n_surv_rec = 0;
 
   void free_list(std::vector<void*>& v) {
@@ -121,6 +122,7 @@ struct mv_engine {
     free_list(prob_allocs);
     for (auto e : ev_var) (void)hipEventDestroy(e);
     for (auto e : ev_mlp) (void)hipEventDestroy(e);
+    for (auto e : ev_cons) (void)hipEventDestroy(e);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
@@ -217,19 +219,74 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     K((double**)&p.mlS, ms.data(), Dm4);
     K((double**)&p.mlM, mm.data(), Dm4);
   }
-  K((int**)&p.op_code, pd->op_code, C);
-  K((int**)&p.op_arg, pd->op_arg, (size_t)C * 4);
-  K((double**)&p.op_k, pd->op_karg, (size_t)C * 2);
+  // constraint program sorted by op code (lane-uniform branches), ABS_SUMDIFF ops last
+  std::vector<int> order(C);
+  for (int c = 0; c < C; ++c) order[c] = c;
+  auto key = [&](int c) { return pd->op_code[c] == MV_OP_ABS_SUMDIFF ? 1 << 20 : pd->op_code[c]; };
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key(x) < key(y); });
+  std::vector<int> scode(C), sarg((size_t)C * 4), scol(C);
+  std::vector<double> sk((size_t)C * 2);
+  int n_sd = 0;
+  for (int k = 0; k < C; ++k) {
+    const int c = order[k];
+    scode[k] = pd->op_code[c];
+    scol[k] = c;
+    for (int q = 0; q < 4; ++q) sarg[(size_t)k * 4 + q] = pd->op_arg[(size_t)c * 4 + q];
+    for (int q = 0; q < 2; ++q) sk[(size_t)k * 2 + q] = pd->op_karg[(size_t)c * 2 + q];
+    n_sd += scode[k] == MV_OP_ABS_SUMDIFF;
+  }
+  K((int**)&p.op_code, scode.data(), C);
+  K((int**)&p.op_arg, sarg.data(), (size_t)C * 4);
+  K((double**)&p.op_k, sk.data(), (size_t)C * 2);
+  K((int**)&p.op_col, scol.data(), C);
   K((int**)&p.idx_pool, pd->idx_pool, pd->n_pool);
-  std::vector<int> sdo;
-  for (int c = 0; c < C; ++c)
-    if (pd->op_code[c] == MV_OP_ABS_SUMDIFF) sdo.push_back(c);
-  p.n_sumdiff = (int)sdo.size();
+  p.n_pool = pd->n_pool;
+  p.n_sumdiff = n_sd;
   p.full_ops = 0;
   for (int c = 0; c < C; ++c)
     if (pd->op_code[c] >= MV_OP_LCLD_INSTALL && pd->op_code[c] <= MV_OP_RATIO_MASKED)
       p.full_ops = 1;
-  K((int**)&p.sumdiff_ops, sdo.data(), sdo.size());
+  p.ident = V == Dm;
+  for (int g = 0; g < V && p.ident; ++g)
+    p.ident = pd->gene_kind[g] != MV_GENE_OHE && pd->gene_feat[g] == pd->mut_feats[g];
+  if (V > VARY_MAX_V || p.Dm4 > VARY_MAX_V) {
+    delete e;
+    return fail(MV_ERR_ARG, "genetic length / mutable features must be <= 1024");
+  }
+  {  // k_vary problem blob: the LDS image of the tables (kernels.h vary_offsets)
+    const VaryOff vo = vary_offsets(p);
+    if (gen_lds(vo, false, false, true).total > 160 * 1024 || cons_lds_total(vo) > 160 * 1024) {
+      delete e;
+      return fail(MV_ERR_ARG, "problem too large for the k_vary LDS workspace");
+    }
+    std::vector<unsigned char> blob(vo.vb, 0);
+    auto put = [&](unsigned off, const void* src, size_t n) {
+      if (n) std::memcpy(blob.data() + off, src, n);
+    };
+    put(vo.opa, sarg.data(), (size_t)C * 16);
+    put(vo.opk, sk.data(), (size_t)C * 16);
+    std::vector<double> ms(p.Dm4, 0.0), mm(p.Dm4, 0.0);
+    for (int j = 0; j < Dm; ++j) {
+      ms[j] = mls[pd->mut_feats[j]];
+      mm[j] = mlm[pd->mut_feats[j]];
+    }
+    put(vo.mlS, ms.data(), (size_t)p.Dm4 * 8);
+    put(vo.mlM, mm.data(), (size_t)p.Dm4 * 8);
+    put(vo.opc, scode.data(), (size_t)C * 4);
+    put(vo.ocol, scol.data(), (size_t)C * 4);
+    put(vo.pool, pd->idx_pool, (size_t)pd->n_pool * 4);
+    put(vo.ginfo, info.data(), (size_t)V4 * 4);
+    put(vo.mutf, pd->mut_feats, (size_t)Dm * 4);
+    // mutation gap table T[k] = floor((1 - 1/V)^k 2^32), k = 0..V (oracle geometric_table)
+    std::vector<uint32_t> geo(V + 1);
+    const double q = 1.0 - 1.0 / (double)V;
+    for (int k = 0; k <= V; ++k) {
+      const double t = std::floor(std::pow(q, (double)k) * 4294967296.0);
+      geo[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    }
+    put(vo.geo, geo.data(), (size_t)(V + 1) * 4);
+    K((unsigned char**)&p.vblob, blob.data(), blob.size());
+  }
   p.tol = pd->tol;
   p.norm = pd->norm;
   p.scale_obj = pd->scale_objectives;
@@ -311,17 +368,16 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
   K((int**)&s.min_class, minimize_class, B);
   K((double**)&s.gl, (const double*)nullptr, (size_t)B * p.V);
   K((double**)&s.gu, (const double*)nullptr, (size_t)B * p.V);
-  K((double**)&s.enc_scale, (const double*)nullptr, (size_t)B * p.Dm);
-  K((double**)&s.enc_min, (const double*)nullptr, (size_t)B * p.Dm);
-  K((double**)&s.x0_mm, (const double*)nullptr, (size_t)B * p.Dm);
+  K((unsigned char**)&s.sblob, (const unsigned char*)nullptr,
+    (size_t)B * vary_offsets(p).sb);
   K((float**)&s.bias1, (const float*)nullptr, (size_t)B * e->H1);
   K(&e->genes0, (const double*)nullptr, (size_t)B * p.V);
   if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
   int slot = 0;
   HIPCHK(stage_rows(base_rows(e), (hipStream_t)stream, &slot));
   HIPCHK(launch_setup_states(slot, B, s.x_init, dxl, dxu, e->W1full, e->b1, (double*)s.gl,
-                             (double*)s.gu, (double*)s.enc_scale, (double*)s.enc_min,
-                             (double*)s.x0_mm, (float*)s.bias1, e->genes0, (hipStream_t)stream));
+                             (double*)s.gu, (unsigned char*)s.sblob, (float*)s.bias1, e->genes0,
+                             (hipStream_t)stream));
   HIPCHK(release_rows(slot, (hipStream_t)stream));
   e->B = B;
   return MV_OK;
@@ -474,7 +530,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     HIPCHK(hipDeviceSynchronize());
     e->free_list(e->attack_allocs);
     e->d_phase = nullptr;
-    hipError_t err = hipSuccess;
+      hipError_t err = hipSuccess;
     auto A = [&](auto** dst, size_t n) {
       if (err != hipSuccess) return;
       err = dalloc(dst, n);
@@ -564,6 +620,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   if (e->profiling) {
     if (ensure_events(e->ev_var, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_mlp, (size_t)G) != MV_OK) return MV_ERR_HIP;
+    if (ensure_events(e->ev_cons, (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_surv, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
   }
   e->n_var_rec = 0;
@@ -590,7 +647,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   for (int g = 1; g < G; ++g) {
     const int hist_row0 = P + (g - 1) * O;
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], stream));
-    HIPCHK(launch_vary(va, slot_va, g, hist_row0, stream));
+    HIPCHK(launch_gen(va, slot_va, g, hist_row0, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], stream));
+    HIPCHK(launch_cons(va, slot_va, hist_row0, stream));
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], stream));
     HIPCHK(launch_mlp(va, slot_va, hist_row0, stream));
     if (e->profiling) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], stream));
@@ -647,6 +706,30 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
                  afast / e->B, nflag / e->B);
     std::fprintf(stderr, "\n");
   }
+  return MV_OK;
+}
+
+int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations) {
+  if (!e || !ms) return fail(MV_ERR_ARG, "null argument");
+  double t[4] = {0, 0, 0, 0};
+  for (int i = 0; i < e->n_var_rec; ++i) {
+    float a = 0.f, b = 0.f, c = 0.f;
+    HIPCHK(hipEventSynchronize(e->ev_mlp[i]));
+    HIPCHK(hipEventElapsedTime(&a, e->ev_var[2 * i], e->ev_cons[i]));
+    HIPCHK(hipEventElapsedTime(&b, e->ev_cons[i], e->ev_var[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&c, e->ev_var[2 * i + 1], e->ev_mlp[i]));
+    t[0] += a;
+    t[1] += b;
+    t[2] += c;
+  }
+  for (int i = 0; i < e->n_surv_rec; ++i) {
+    float s = 0.f;
+    HIPCHK(hipEventSynchronize(e->ev_surv[2 * i + 1]));
+    HIPCHK(hipEventElapsedTime(&s, e->ev_surv[2 * i], e->ev_surv[2 * i + 1]));
+    t[3] += s;
+  }
+  for (int k = 0; k < 4; ++k) ms[k] = t[k];
+  if (n_generations) *n_generations = e->n_var_rec < e->n_surv_rec ? e->n_var_rec : e->n_surv_rec;
   return MV_OK;
 }
 

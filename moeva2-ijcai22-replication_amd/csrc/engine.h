@@ -18,6 +18,9 @@ namespace mv {
 constexpr int MAX_LAYERS = 6;
 constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
 constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
+constexpr int VARY_T = 256;      // threads per k_vary workgroup (4 waves, one row buffer each)
+constexpr int VARY_MAX_ROWS = 256;  // rows per k_vary workgroup (<= 64 per wave)
+constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
 constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS
 constexpr int SURV_RMAX = 640;   // reference points
@@ -38,13 +41,18 @@ struct DProblem {
   const double* ml_min;   // [D]
   const double* mlS;      // [Dm4] ml_scale gathered at the mutable features
   const double* mlM;      // [Dm4] ml_min   gathered at the mutable features
+  // constraint program, ops sorted by code (lane-uniform branches), ABS_SUMDIFF ops last
   const int* op_code;     // [C]
   const int* op_arg;      // [C*4]
   const double* op_k;     // [C*2]
+  const int* op_col;      // [C] original constraint column of each sorted op
   const int* idx_pool;
-  int n_sumdiff;          // ABS_SUMDIFF ops, evaluated wave-parallel
+  int n_pool;
+  int n_sumdiff;          // ABS_SUMDIFF ops (positions C - n_sumdiff .. C-1), wave-parallel
+  // k_vary LDS images (kernels.h vary_offsets): problem blob [vb] and per-state blobs [sb]
+  const unsigned char* vblob;
   int full_ops;           // program uses the LCLD financial ops (codes 4..8)
-  const int* sumdiff_ops; // [n_sumdiff] their column indices
+  int ident;              // V == Dm, no one-hot genes, gene g <-> mutable feature g
   double tol;
   int norm;               // 2 or 0 (inf)
   int scale_obj;
@@ -61,9 +69,8 @@ struct DStates {
   const double* x_init;     // [B][D]
   const double* gl;         // [B][V]
   const double* gu;         // [B][V]
-  const double* enc_scale;  // [B][Dm]
-  const double* enc_min;    // [B][Dm]
-  const double* x0_mm;      // [B][Dm]
+  const unsigned char* sblob;  // [B][sb]: encoder scale/min and scaled origin at the
+                               // mutable features [Dm4] each, then x_init [D] (kernels.h)
   const float* bias1;       // [B][H1]
   const int* min_class;     // [B]
 };

@@ -78,10 +78,45 @@ hipError_t release_rows(int slot, hipStream_t stream) {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// Wave-wide reductions without LDS: DPP within rows of 16 lanes (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror), then gfx950 permlane16/32 swaps across rows.  Every step
+// combines a lane's value with exactly one partner's (commutative), so all 64 lanes end
+// with the same, deterministic total.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+
+// (value of this lane's row-pair partner half, own half) across 16-lane rows (SWAP=16) or
+// 32-lane halves (SWAP=32): returns {x_first, x_second} with x_first + x_second the pair.
+template <int SWAP>
+__device__ __forceinline__ void swap_f64(double v, double& d0, double& d1) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  if (SWAP == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    d0 = __hiloint2double(b[0], a[0]);
+    d1 = __hiloint2double(b[1], a[1]);
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    d0 = __hiloint2double(b[0], a[0]);
+    d1 = __hiloint2double(b[1], a[1]);
+  }
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = v + dpp_f64<0xB1>(v);
+  v = v + dpp_f64<0x4E>(v);
+  v = v + dpp_f64<0x141>(v);
+  v = v + dpp_f64<0x140>(v);
+  double d0, d1;
+  swap_f64<16>(v, d0, d1);
+  v = d0 + d1;
+  swap_f64<32>(v, d0, d1);
+  return d0 + d1;
 }
 
 __device__ __forceinline__ double nanmax(double a, double b) {
@@ -91,9 +126,15 @@ __device__ __forceinline__ double nanmax(double a, double b) {
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = nanmax(v, __shfl_xor(v, o, 64));
-  return v;
+  v = nanmax(v, dpp_f64<0xB1>(v));
+  v = nanmax(v, dpp_f64<0x4E>(v));
+  v = nanmax(v, dpp_f64<0x141>(v));
+  v = nanmax(v, dpp_f64<0x140>(v));
+  double d0, d1;
+  swap_f64<16>(v, d0, d1);
+  v = nanmax(d0, d1);
+  swap_f64<32>(v, d0, d1);
+  return nanmax(d0, d1);
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -117,21 +158,46 @@ __device__ __forceinline__ double month_of(double f) {
   return floor(f / 100.0) * 12.0 + py_mod(f, 100.0);
 }
 
+// Constraint-program tables (ops sorted by code, ABS_SUMDIFF last): global memory
+// (k_constraints) or the LDS copy of the problem blob (k_vary).
+struct OpTab {
+  const int* code;      // [C]
+  const int4* arg;      // [C]
+  const double2* k;     // [C]
+  const int* col;       // [C] original constraint column
+  const int* pool;      // [n_pool]
+  int C, n_lane;        // ops [0, n_lane) lane-parallel, [n_lane, C) ABS_SUMDIFF
+  double tol;
+};
+
+__device__ __forceinline__ OpTab global_tab(const DProblem& p) {
+  OpTab t;
+  t.code = p.op_code;
+  t.arg = (const int4*)p.op_arg;
+  t.k = (const double2*)p.op_k;
+  t.col = p.op_col;
+  t.pool = p.idx_pool;
+  t.C = p.C;
+  t.n_lane = p.C - p.n_sumdiff;
+  t.tol = p.tol;
+  return t;
+}
+
 // One constraint column on the ML row x (LDS).  FULL adds the LCLD financial identities;
 // ABS_SUMDIFF columns are evaluated wave-parallel (sumdiff_wave) by the caller.
 template <bool FULL>
-__device__ __forceinline__ double eval_op(const DProblem& p, int c, const double* __restrict__ x) {
-  const int code = p.op_code[c];
-  const int4 ar = *(const int4*)(p.op_arg + 4 * c);
+__device__ __forceinline__ double eval_op(const OpTab& t, int c, const double* __restrict__ x) {
+  const int code = t.code[c];
+  const int4 ar = t.arg[c];
   switch (code) {
     case 1:  // MV_OP_DIFF (botnet_constraints.py:283-285)
       return x[ar.x] - x[ar.y];
     case 2: {  // MV_OP_RATIO_SAFE (botnet_constraints.py:304-306)
       const double a = x[ar.x], b = x[ar.y];
-      return (b != 0.0 ? a / b : 0.0) - p.op_k[2 * c];
+      return (b != 0.0 ? a / b : 0.0) - t.k[c].x;
     }
     case 9: {  // MV_OP_XOR_AUG (examples/utils.py:7-29)
-      const double2 k = *(const double2*)(p.op_k + 2 * c);
+      const double2 k = t.k[c];
       const bool b1 = x[ar.y] >= k.x;
       const bool b2 = x[ar.z] >= k.y;
       return fabs(x[ar.x] - ((b1 != b2) ? 1.0 : 0.0));
@@ -147,11 +213,11 @@ __device__ __forceinline__ double eval_op(const DProblem& p, int c, const double
         const double base = 1.0 + x2 / 1200.0;
         const double num = (x0 * r) * pow(base, x1);
         const double den = pow(base, x1) - 1.0;
-        return fabs(x3 - num / den) - p.op_k[2 * c];
+        return fabs(x3 - num / den) - t.k[c].x;
       }
       case 5: {  // MV_OP_LCLD_TERM (:186)
-        const double t = x[ar.x];
-        return fabs((36.0 - t) * (60.0 - t));
+        const double v = x[ar.x];
+        return fabs((36.0 - v) * (60.0 - v));
       }
       case 6:  // MV_OP_ABS_RATIO (:189-207)
         return fabs(x[ar.x] - x[ar.y] / x[ar.z]);
@@ -173,47 +239,108 @@ __device__ __forceinline__ double eval_op(const DProblem& p, int c, const double
   return __builtin_nan("");
 }
 
-// |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes (exact for the integer-valued
-// features of every shipped program; summation order differs from numpy otherwise).
-__device__ __forceinline__ double sumdiff_wave(const DProblem& p, int c, const double* x,
-                                               int lane) {
-  const int4 ar = *(const int4*)(p.op_arg + 4 * c);
-  double s0 = 0.0, s1 = 0.0;
-  for (int q = ar.x + lane; q < ar.y; q += 64) s0 += x[p.idx_pool[q]];
-  for (int q = ar.y + lane; q < ar.z; q += 64) s1 += x[p.idx_pool[q]];
-  s0 = wave_sum(s0);
-  s1 = wave_sum(s1);
-  return fabs(s0 - s1);
+// |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes, one reduction of the per-lane
+// differences (exact for the integer-valued features of every shipped program; the
+// summation order differs from numpy otherwise).
+__device__ __forceinline__ double sumdiff_wave(const OpTab& t, int c, const double* x, int lane) {
+  const int4 ar = t.arg[c];
+  double s = 0.0;
+  for (int q = ar.x + lane; q < ar.y; q += 64) s += x[t.pool[q]];
+  for (int q = ar.y + lane; q < ar.z; q += 64) s -= x[t.pool[q]];
+  return fabs(wave_sum(s));
 }
 
 // Constraint row -> G columns (+ history columns); returns the wave-uniform f3 = sum(G).
 // Values <= tol -> 0 (Constraints.evaluate); with clamp, G * (G > 0) (default_problem.py:93-97).
 template <bool FULL>
-__device__ __forceinline__ double constraints_row(const DProblem& p, const double* xrow,
-                                                  int lane, double* grow, double* hcols,
+__device__ __forceinline__ double constraints_row(const OpTab& t, const double* xrow, int lane,
+                                                  double* grow, double* hcols,
                                                   bool clamp_positive) {
   double acc3 = 0.0;
-  for (int c = lane; c < p.C; c += 64) {
-    if (p.op_code[c] == 3) continue;
-    double v = eval_op<FULL>(p, c, xrow);
-    if (v <= p.tol) v = 0.0;
+  for (int c = lane; c < t.n_lane; c += 64) {
+    double v = eval_op<FULL>(t, c, xrow);
+    if (v <= t.tol) v = 0.0;
     const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
-    if (grow) grow[c] = g;
-    if (hcols) hcols[c] = g;
+    if (grow) grow[t.col[c]] = g;
+    if (hcols) hcols[t.col[c]] = g;
     acc3 += g;
   }
-  for (int k = 0; k < p.n_sumdiff; ++k) {
-    const int c = p.sumdiff_ops[k];
-    double v = sumdiff_wave(p, c, xrow, lane);
-    if (v <= p.tol) v = 0.0;
+  for (int c = t.n_lane; c < t.C; ++c) {
+    double v = sumdiff_wave(t, c, xrow, lane);
+    if (v <= t.tol) v = 0.0;
     const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
     if (lane == 0) {
-      if (grow) grow[c] = g;
-      if (hcols) hcols[c] = g;
+      if (grow) grow[t.col[c]] = g;
+      if (hcols) hcols[t.col[c]] = g;
       acc3 += g;
     }
   }
   return wave_sum(acc3);
+}
+
+// k_vary's constraint evaluation: each lane keeps its (at most OPS_REG) lane-parallel ops
+// packed in registers -- code (4 bits) | a0 (14) | a1 (14) -- so a row's operand reads are
+// independent LDS loads issued back to back.  DIFF and RATIO_SAFE (the botnet program) are
+// evaluated inline; other codes, and ops beyond OPS_REG per lane, go through eval_op.
+constexpr int OPS_REG = 8;
+
+__device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
+  const int4 ar = t.arg[c];
+  return (unsigned)t.code[c] | ((unsigned)ar.x << 4) | ((unsigned)ar.y << 18);
+}
+
+template <bool FULL>
+__device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigned* opw, int kops,
+                                                   const double* xrow, int lane, double* grow,
+                                                   double* hcols) {
+  double va[OPS_REG], vb[OPS_REG];
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    if (k < kops) {
+      va[k] = xrow[(opw[k] >> 4) & 0x3FFF];
+      vb[k] = xrow[opw[k] >> 18];
+    }
+  }
+  double acc3 = 0.0;
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    const int c = lane + 64 * k;
+    if (k < kops && c < t.n_lane) {
+      const int code = opw[k] & 15;
+      double v;
+      if (code == 1)
+        v = va[k] - vb[k];
+      else if (code == 2)
+        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k[c].x;
+      else
+        v = eval_op<FULL>(t, c, xrow);
+      if (v <= t.tol) v = 0.0;
+      const double g = v * (v > 0.0 ? 1.0 : 0.0);
+      if (grow) grow[t.col[c]] = g;
+      if (hcols) hcols[t.col[c]] = g;
+      acc3 += g;
+    }
+  }
+  for (int c = lane + 64 * OPS_REG; c < t.n_lane; c += 64) {
+    double v = eval_op<FULL>(t, c, xrow);
+    if (v <= t.tol) v = 0.0;
+    const double g = v * (v > 0.0 ? 1.0 : 0.0);
+    if (grow) grow[t.col[c]] = g;
+    if (hcols) hcols[t.col[c]] = g;
+    acc3 += g;
+  }
+  double sdsum = 0.0;  // ABS_SUMDIFF columns (wave-uniform values)
+  for (int c = t.n_lane; c < t.C; ++c) {
+    double v = sumdiff_wave(t, c, xrow, lane);
+    if (v <= t.tol) v = 0.0;
+    const double g = v * (v > 0.0 ? 1.0 : 0.0);
+    if (lane == 0) {
+      if (grow) grow[t.col[c]] = g;
+      if (hcols) hcols[t.col[c]] = g;
+    }
+    sdsum += g;
+  }
+  return wave_sum(acc3) + sdsum;
 }
 
 // pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction.
@@ -237,36 +364,28 @@ __device__ __forceinline__ double poly_mut(double x, double xl, double xu, doubl
   return y;
 }
 
-struct Cx {
-  int on[2];
-  int lo[2];
-  int hi[2];
+// Crossover draws of one mating for one variable-type subset (oracle crossover_draws):
+// on = u53 < prob; genes of the subset with index in [lo, hi) are swapped.
+struct CxSub {
+  int on, lo, hi;
 };
 
-// Crossover draws of mating m for both variable-type subsets (oracle crossover_draws).
-__device__ __forceinline__ Cx cx_draws(const Rng& rng, int gen, int m, const int n_sub[2],
-                                       double prob) {
-  Cx c;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int n = n_sub[s];
-    c.on[s] = 0;
-    c.lo[s] = 0;
-    c.hi[s] = 0;
-    if (n <= 0) continue;
-    const u32x4 w = rng.draw((uint32_t)(m * 2 + s), (uint32_t)gen, TAG_CX);
-    c.on[s] = u53(w.x, w.y) < prob;
-    if (n - 1 <= 0) continue;
-    const int a = 1 + (int)(((uint64_t)w.z * (uint64_t)(n - 1)) >> 32);
-    if (n - 1 == 1) {
-      c.lo[s] = a;
-      c.hi[s] = n;
-    } else {
-      int b = 1 + (int)(((uint64_t)w.w * (uint64_t)(n - 2)) >> 32);
-      if (b >= a) ++b;
-      c.lo[s] = a < b ? a : b;
-      c.hi[s] = a < b ? b : a;
-    }
+__device__ __forceinline__ CxSub cx_sub(const Rng& rng, int gen, int m, int s, int n,
+                                        double prob) {
+  CxSub c{0, 0, 0};
+  if (n <= 0) return c;
+  const u32x4 w = rng.draw((uint32_t)(m * 2 + s), (uint32_t)gen, TAG_CX);
+  c.on = u53(w.x, w.y) < prob;
+  if (n - 1 <= 0) return c;
+  const int a = 1 + (int)(((uint64_t)w.z * (uint64_t)(n - 1)) >> 32);
+  if (n - 1 == 1) {
+    c.lo = a;
+    c.hi = n;
+  } else {
+    int b = 1 + (int)(((uint64_t)w.w * (uint64_t)(n - 2)) >> 32);
+    if (b >= a) ++b;
+    c.lo = a < b ? a : b;
+    c.hi = a < b ? b : a;
   }
   return c;
 }
@@ -283,141 +402,458 @@ __device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restri
   }
 }
 
-// Generate (mode 1) or load (mode 0) the genes of row (b, i); lane-parallel, 4 genes/lane.
-// gene_info packs kind (2 bits) | subset index << 2 | feature (or OHE group) << 17.
-__device__ __forceinline__ void row_genes(const RowsArgs& a, int gen, int b, int i, int lane,
-                                          double* xrow) {
+__device__ __forceinline__ int rdl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+// Geometric gap of the mutation process (oracle mutation_draws): the number of
+// non-mutated genes before the next mutated one is the largest k in [0, V] with
+// w < T[k], T[k] = floor((1 - 1/V)^k * 2^32) (T[0] unused), found by binary search.
+__device__ __forceinline__ int geo_gap(const uint32_t* T, int V, uint32_t w, float lq) {
+  // estimate from log2(w / 2^32) / log2(1 - 1/V), then step to the exact table answer
+  int k = (int)(__log2f(((float)w + 0.5f) * 2.3283064365386963e-10f) / lq);
+  k = k < 0 ? 0 : (k > V ? V : k);
+  while (k < V && w < T[k + 1]) ++k;
+  while (k > 0 && !(w < T[k])) --k;
+  return k;
+}
+
+// MixedVariableMutation of one gene (moeva2.py:104-111): real_pm, or int_pm =
+// IntegerFromFloatMutation (bounds widened by 0.5 - 1e-16, np.round half-to-even, clamp).
+__device__ __forceinline__ double mutate_gene(double x, double xl, double xu, bool is_real,
+                                              double u, double eta) {
+  const double y = poly_mut(x, is_real ? xl : xl - INT_WIDEN, is_real ? xu : xu + INT_WIDEN, u,
+                            eta);
+  if (is_real) return y;
+  double yi = rint(y);
+  if (yi < xl) yi = xl;
+  if (yi > xu) yi = xu;
+  return yi;
+}
+
+__device__ __forceinline__ bool gene_swapped(int info, int on0, int lo0, int hi0, int on1,
+                                             int lo1, int hi1) {
+  const int sub = (info >> 2) & 0x7FFF;
+  return (info & 3) == 0 ? (on0 && sub >= lo0 && sub < hi0) : (on1 && sub >= lo1 && sub < hi1);
+}
+
+constexpr int MUT_CAP = 4;     // mutations per row precomputed in the prologue (registers)
+constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream (V <= 1024)
+
+// Crossover draws of one subset packed into one word: on | lo << 1 | hi << 16.
+__device__ __forceinline__ int pack_cx(const CxSub& c) { return c.on | (c.lo << 1) | (c.hi << 16); }
+__device__ __forceinline__ bool swapped_packed(int info, int cx0, int cx1) {
+  const int sub = (info >> 2) & 0x7FFF;
+  const int c = (info & 3) == 0 ? cx0 : cx1;
+  return (c & 1) && sub >= ((c >> 1) & 0x7FFF) && sub < (c >> 16);
+}
+__device__ __forceinline__ double rdl_d(double v, int k) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
+  return __hiloint2double(hi, lo);
+}
+
+// Async global -> LDS copy of nbytes (a 1-KiB multiple): 16 B per lane, 1 KiB per wave
+// instruction, the workgroup's waves interleaved.
+__device__ __forceinline__ void glds_copy(unsigned char* lds, const unsigned char* g,
+                                          unsigned nbytes, int wave, int lane) {
+  for (unsigned off = wave * 1024u; off < nbytes; off += VARY_T * 16u)
+    __builtin_amdgcn_global_load_lds(g + off + lane * 16, lds + off, 16, 0, 0);
+}
+
+// Rows of one k_gen / k_cons workgroup: a chunk of one state's rows; wave w takes rows
+// i0 + w + 4k (k < nrw).
+struct RowChunk {
+  int b, i0, i1, nrw;
+};
+__device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
+  RowChunk r;
+  const int nchunk = (n + rows_wg - 1) / rows_wg;
+  r.b = blockIdx.x / nchunk;
+  r.i0 = (blockIdx.x - r.b * nchunk) * rows_wg;
+  r.i1 = min(n, r.i0 + rows_wg);
+  const int span = r.i1 - r.i0 - wave;
+  r.nrw = span > 0 ? (span + 3) / 4 : 0;
+  return r;
+}
+
+// k_gen: variation (mode 1) or gene load (mode 0), the child genes to the pool, the fp32
+// ML-scaled mutable row for k_mlp (default_problem.py:119-121) and f2, the encoder-MinMax
+// distance (default_problem.py:80-91).
+//
+// Lane l owns genes l + 64t: coalesced 512-B gene loads/stores, its gene-table words (and,
+// REGC, its ML-scaler / encoder coefficients) in registers; the next row's parent genes
+// are loaded while the current row is finished.  Two-point crossover draws and the
+// mutations are precomputed for all of a wave's rows at once, one row per lane: mutations
+// are a geometric-gap process (about two Philox draws per row instead of one word per
+// gene), at most MUT_CAP per row cached in registers, the rare rest finished in the row.
+template <bool IDENT, int NT>
+__global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
+  constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
-  const int V = p.V;
-  double* gout = nullptr;
-  if (a.genes_out) {
-    const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
-    gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const RowChunk rc = row_chunk(a.n, rows_wg, wave);
+  const int b = rc.b, nrw = rc.nrw;
+  const int V = p.V, Dm = p.Dm, Dm4 = p.Dm4;
+  const bool ev = a.do_eval != 0;
+  const VaryOff o = vary_offsets(p);
+  const GenLds L = gen_lds(o, REGC, IDENT, ev);
+  const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
+  glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
+  if (ev && !REGC) {
+    glds_copy(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
+    glds_copy(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
   }
-  if (a.mode == 0) {
-    const double* gin = a.genes_in + ((size_t)b * a.in_rows + i) * V;
-    for (int g = lane; g < V; g += 64) {
-      const double x = gin[g];
-      if (gout) gout[g] = x;
-      if (xrow) scatter_gene(p, xrow, p.gene_info[g], x);
-    }
-    return;
-  }
-  const Rng rng(a.seed, a.stream_key);
-  const int nm = a.n / 2;
-  const int m = i % nm;
-  const int side = i / nm;
-  const int* par = a.parents + ((size_t)b * nm + m) * 2;
-  const int own = side ? par[1] : par[0];
-  const int oth = side ? par[0] : par[1];
-  const double* gown = a.genes_in + ((size_t)b * a.in_rows + own) * V;
-  const double* goth = a.genes_in + ((size_t)b * a.in_rows + oth) * V;
-  const Cx cx = cx_draws(rng, gen, m, p.n_sub, a.cx_prob);
-  const int nq = (V + 3) >> 2;
-  const double* gl = a.s.gl + (size_t)b * V;
-  const double* gu = a.s.gu + (size_t)b * V;
-  for (int g0 = lane * 4; g0 < V; g0 += 256) {
-    const int4 inf4 = *(const int4*)(p.gene_info + g0);  // padded to a multiple of 4
-    const u32x4 w = rng.draw((uint32_t)(i * nq + (g0 >> 2)), (uint32_t)gen, TAG_MUT_MASK);
-    const int infs[4] = {inf4.x, inf4.y, inf4.z, inf4.w};
-    const uint32_t words[4] = {w.x, w.y, w.z, w.w};
-    double xv[4];
+  if (ev && !IDENT) glds_copy(smem + L.x_at, sblob, o.x_end, wave, lane);
+  // per-lane gene-table words and (REGC) coefficients, straight from HBM meanwhile
+  int ginf[NT];
+  double cS[NT], cM[NT], cE[NT], cN[NT], cX[NT];
+  {
+    const int* gi = (const int*)(p.vblob + o.ginfo);
+    const double* mS = (const double*)(p.vblob + o.mlS);
+    const double* mM = (const double*)(p.vblob + o.mlM);
+    const double* sE = (const double*)(sblob + o.es);
+    const double* sN = (const double*)(sblob + o.em);
+    const double* sX = (const double*)(sblob + o.x0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int info = infs[j];
-      const int ss = (info & 3) == 0 ? 0 : 1;
-      const int sub = (info >> 2) & 0x7FFF;
-      const bool swap = cx.on[ss] && sub >= cx.lo[ss] && sub < cx.hi[ss];
-      xv[j] = (g0 + j < V) ? (swap ? goth : gown)[g0 + j] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int g = g0 + j;
-      if (g < V) {
-        double x = xv[j];
-        if (words[j] < a.mut_thr) {  // prob 1/V: one lane per row on average
-          const bool is_real = (infs[j] & 3) == 0;
-          const u32x4 wu = rng.draw((uint32_t)(i * V + g), (uint32_t)gen, TAG_MUT_U);
-          const double xl = gl[g], xu = gu[g];
-          const double y = poly_mut(x, is_real ? xl : xl - INT_WIDEN,
-                                    is_real ? xu : xu + INT_WIDEN, u53(wu.x, wu.y), a.eta);
-          if (is_real) {
-            x = y;
-          } else {  // IntegerFromFloatMutation: np.round (half to even), then clamp
-            double yi = rint(y);
-            if (yi < xl) yi = xl;
-            if (yi > xu) yi = xu;
-            x = yi;
-          }
-        }
-        if (gout) gout[g] = x;
-        if (xrow) scatter_gene(p, xrow, infs[j], x);
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      ginf[t] = g < V ? gi[g] : 0;
+      if (REGC) {
+        const bool in = ev && g < Dm4;
+        cS[t] = in ? mS[g] : 0.0;
+        cM[t] = in ? mM[g] : 0.0;
+        cE[t] = in ? sE[g] : 0.0;
+        cN[t] = in ? sN[g] : 0.0;
+        cX[t] = in ? sX[g] : 0.0;
       }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
+  const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
+  const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
+  const double* s_mlS = (const double*)(smem + L.c_at + (o.mlS - o.c_at));
+  const double* s_mlM = (const double*)(smem + L.c_at + (o.mlM - o.c_at));
+  const double* s_es = (const double*)(smem + L.e_at + (o.es - o.e_at));
+  const double* s_em = (const double*)(smem + L.e_at + (o.em - o.e_at));
+  const double* s_x0 = (const double*)(smem + L.e_at + (o.x0 - o.e_at));
+  double* xrow = (double*)(smem + L.rows_at + wave * o.rb);
+  if (ev && !IDENT) {  // immutable features of this wave's row buffer (written once)
+    const double* s_xi = (const double*)(smem + L.x_at);
+    for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
+  }
+
+  // this wave's rows: lane k holds row k's packed parents (own | oth << 16), crossover
+  // draws, destination and mutations (count | overflow << 3 | (last position + 1) << 4)
+  int par_v = 0, cx0_v = 0, cx1_v = 0, orow_v = 0, mut_v = 0;
+  int mpos[MUT_CAP];
+  double mval[MUT_CAP];
+#pragma unroll
+  for (int q = 0; q < MUT_CAP; ++q) {
+    mpos[q] = -1;
+    mval[q] = 0.0;
+  }
+  const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
+  const bool mine = lane < nrw;
+  const int irow = rc.i0 + wave + 4 * lane;
+  if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
+  if (a.mode == 1) {
+    const Rng rng(a.seed, a.stream_key);
+    if (mine) {
+      const int nm = a.n / 2;
+      const int m = irow % nm;
+      const int side = irow / nm;
+      const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
+      par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
+      cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
+      cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
+    }
+    // (1) mutation positions and their PM uniforms
+    const float lq = __log2f(1.0f - 1.0f / (float)V);
+    bool going = mine;
+    int pos = -1, cnt = 0, ovf = 0;
+    double mu[MUT_CAP];
+#pragma unroll 1
+    for (int j = 0; j <= MUT_CAP && __ballot(going); ++j) {
+      bool have = false;
+      double u = 0.0;
+      if (going) {
+        const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+        pos += 1 + geo_gap(s_geo, V, w.x, lq);
+        if (pos >= V) {
+          going = false;
+        } else if (j == MUT_CAP) {
+          ovf = 1;
+          going = false;
+        } else {
+          have = true;
+          u = u53(w.y, w.z);
+          cnt = j + 1;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < MUT_CAP; ++q)
+        if (have && q == j) {
+          mpos[q] = pos;
+          mu[q] = u;
+        }
+    }
+    // (2) crossed parent values at those positions (independent loads), (3) mutate
+#pragma unroll
+    for (int q = 0; q < MUT_CAP; ++q) {
+      if (q < cnt) {
+        const bool sw = swapped_packed(s_ginfo[mpos[q]], cx0_v, cx1_v);
+        mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mpos[q]];
+      }
+    }
+    const double* gl = a.s.gl + (size_t)b * V;
+    const double* gu = a.s.gu + (size_t)b * V;
+#pragma unroll 1
+    for (int q = 0; q < MUT_CAP && __ballot(q < cnt); ++q) {
+      int gp = 0;
+      double xv = 0.0, u = 0.0;
+#pragma unroll
+      for (int r = 0; r < MUT_CAP; ++r)
+        if (r == q) {
+          gp = mpos[r];
+          xv = mval[r];
+          u = mu[r];
+        }
+      if (q < cnt) {
+        xv = mutate_gene(xv, gl[gp], gu[gp], (s_ginfo[gp] & 3) == 0, u, a.eta);
+#pragma unroll
+        for (int r = 0; r < MUT_CAP; ++r)
+          if (r == q) mval[r] = xv;
+      }
+    }
+    int last = -1;
+#pragma unroll
+    for (int q = 0; q < MUT_CAP; ++q)
+      if (q < cnt) last = mpos[q];
+    mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
+  } else if (mine) {
+    par_v = irow | (irow << 16);
+  }
+  auto load_row = [&](int k, double* x) {
+    int Vo = V;
+    asm volatile("" : "+s"(Vo));  // keep the per-t bounds out of loop-invariant hoisting
+    const int pr = rdl(par_v, k);
+    const int cx0 = rdl(cx0_v, k), cx1 = rdl(cx1_v, k);
+    const double* gown = gin + (size_t)(pr & 0xFFFF) * V;
+    const double* goth = gin + (size_t)(pr >> 16) * V;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      if (g < Vo) x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g];
+    }
+  };
+  const bool l2 = p.norm == 2;
+  // child genes -> pool, fp32 ML row, f2 (row k of this wave, genes already mutated)
+  auto finish_row = [&](int k, const double* x) {
+    int Vo = V, Dmo = Dm, Dm4o = Dm4;
+    asm volatile("" : "+s"(Vo), "+s"(Dmo), "+s"(Dm4o));
+    const int i = rc.i0 + wave + 4 * k;
+    const int orow = rdl(orow_v, k);
+    if (a.genes_out) {
+      double* gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (lane + 64 * t < Vo) gout[lane + 64 * t] = x[t];
+    }
+    if (!ev) return;
+    float* xo = a.xml + ((size_t)b * a.n + i) * Dm4;
+    double acc = 0.0;
+    if (IDENT) {  // gene g <-> mutable feature g: no decoding
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int j = lane + 64 * t;
+        if (j < Dm4o) {
+          float v = 0.f;
+          if (j < Dmo) {
+            const double xf = x[t];
+            const double ms = REGC ? cS[t] : s_mlS[j], mm = REGC ? cM[t] : s_mlM[j];
+            const double es = REGC ? cE[t] : s_es[j], em = REGC ? cN[t] : s_em[j];
+            const double x0 = REGC ? cX[t] : s_x0[j];
+            v = (float)(xf * ms + mm);
+            const double d = (xf * es + em) - x0;
+            acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
+          }
+          xo[j] = v;
+        }
+      }
+    } else {  // decode through the row buffer (feature_encoder.py:91-124)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (lane + 64 * t < V) scatter_gene(p, xrow, ginf[t], x[t]);
+      wave_sync();
+      for (int j = lane; j < Dm4; j += 64) {
+        float v = 0.f;
+        if (j < Dm) {
+          const double xf = xrow[s_mutf[j]];
+          v = (float)(xf * s_mlS[j] + s_mlM[j]);
+          const double d = (xf * s_es[j] + s_em[j]) - s_x0[j];
+          acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
+        }
+        xo[j] = v;
+      }
+      wave_sync();  // the next row's scatter overwrites xrow
+    }
+    acc = l2 ? wave_sum(acc) : wave_max(acc);
+    if (lane == 0) {
+      double f2 = l2 ? sqrt(acc) : acc;
+      if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
+      if (a.F) a.F[((size_t)b * a.out_rows + orow) * 3 + 1] = f2;
+      if (a.hist) a.hist[((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w + 1] = f2;
+    }
+  };
+  double xn[NT];
+  if (nrw > 0) load_row(0, xn);
+  for (int k = 0; k < nrw; ++k) {
+    double x[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) x[t] = xn[t];
+    if (k + 1 < nrw) load_row(k + 1, xn);
+    if (a.mode == 1) {  // apply the row's cached mutations
+      const int nmut = rdl(mut_v, k) & 7;
+#pragma unroll
+      for (int q = 0; q < MUT_CAP; ++q) {
+        if (q < nmut) {
+          const int pos = rdl(mpos[q], k);
+          const double y = rdl_d(mval[q], k);
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            if (pos == lane + 64 * t) x[t] = y;
+        }
+      }
+    }
+    finish_row(k, x);
+  }
+  // Rare: rows with more than MUT_CAP mutations are redone here with every mutation (same
+  // lanes, same addresses, so these stores land after the row loop's).
+  if (a.mode == 1 && __ballot(mut_v & 8)) {
+    const RowsArgs* ap = &a;
+    const uint64_t seed2 = *(volatile const uint64_t*)&ap->seed;
+    const Rng rng2(seed2, a.stream_key);
+    const double* gl = a.s.gl + (size_t)b * V;
+    const double* gu = a.s.gu + (size_t)b * V;
+    const float lq = __log2f(1.0f - 1.0f / (float)V);
+    for (int k = 0; k < nrw; ++k) {
+      if (!(rdl(mut_v, k) & 8)) continue;
+      const int i = rc.i0 + wave + 4 * k;
+      double x[NT];
+      load_row(k, x);
+      int pos = -1;
+      for (int j = 0;; ++j) {
+        const u32x4 w = rng2.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+        pos += 1 + geo_gap(s_geo, V, w.x, lq);
+        if (pos >= V) break;
+        double xv = 0.0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (pos == lane + 64 * t) xv = x[t];
+        if ((pos & 63) == lane) {
+          xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            if (pos == lane + 64 * t) x[t] = xv;
+        }
+      }
+      finish_row(k, x);
     }
   }
 }
 
-// Variation (mode 1) / gene load (mode 0) + decode + f2 + constraints/f3 + fp32 ML row.
-// One wave per row, 4 rows per workgroup; LDS = 4 ML rows (fp64).
-template <bool FULL>
-__global__ __launch_bounds__(256) void k_vary(int slot, int gen,
-                                              int hist_row0) {
+// k_cons: the constraint program of each evaluated row (Constraints.evaluate numpy path +
+// default_problem.py:93-97,128-129) -> f3 (+ G / history columns).  One workgroup = one
+// state x a chunk of its rows, as k_gen; the row's genes (written by k_gen) are scattered
+// into the wave's ML row buffer whose immutable features were written once, then each lane
+// evaluates its (register-packed) ops.
+template <bool FULL, bool IDENT, int NT>
+__global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_wg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int r = blockIdx.x * 4 + wave;
-  if (r >= a.total) return;
-  const int b = r / a.n;
-  const int i = r - b * a.n;
-  if (!a.do_eval) {
-    row_genes(a, gen, b, i, lane, nullptr);
-    return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const RowChunk rc = row_chunk(a.n, rows_wg, wave);
+  const int b = rc.b, nrw = rc.nrw;
+  const int V = p.V;
+  const VaryOff o = vary_offsets(p);
+  glds_copy(smem, p.vblob, o.a_end, wave, lane);
+  glds_copy(smem + o.a_end, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
+  int ginf[NT];
+  {
+    const int* gi = (const int*)(p.vblob + o.ginfo);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) ginf[t] = lane + 64 * t < V ? gi[lane + 64 * t] : 0;
   }
-  const int D = p.D;
-  double* xrow = (double*)smem + (size_t)wave * D;
-  const double* xi = a.s.x_init + (size_t)b * D;
-  for (int f = lane; f < D; f += 64) xrow[f] = xi[f];
-  wave_sync();
-  row_genes(a, gen, b, i, lane, xrow);
-  wave_sync();
-  // fp32 ML row (scratch) + encoder MinMax distance over the mutable features
-  const int Dm = p.Dm, Dm4 = p.Dm4;
-  const double* es = a.s.enc_scale + (size_t)b * Dm;
-  const double* em = a.s.enc_min + (size_t)b * Dm;
-  const double* x0 = a.s.x0_mm + (size_t)b * Dm;
-  float* xo = a.xml + (size_t)r * Dm4;
-  const bool l2 = p.norm == 2;
-  double acc = 0.0;
-  for (int j = lane; j < Dm4; j += 64) {
-    float v = 0.f;
-    if (j < Dm) {
-      const double xf = xrow[p.mut_feat[j]];
-      v = (float)(xf * p.mlS[j] + p.mlM[j]);
-      const double d = (xf * es[j] + em[j]) - x0[j];
-      acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
-    }
-    xo[j] = v;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  double* xrow = (double*)(smem + o.a_end + o.x_end + wave * o.rb);
+  {
+    const double* s_xi = (const double*)(smem + o.a_end + o.xi);
+    for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
   }
-  acc = l2 ? wave_sum(acc) : wave_max(acc);
-  double f2 = l2 ? sqrt(acc) : acc;
-  if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-  double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-  double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
-  const double f3 = constraints_row<FULL>(p, xrow, lane, grow,
-                                          (hrow && a.hist_w > 3) ? hrow + 3 : nullptr, true);
-  if (lane == 0) {
-    if (a.F) {
-      const int orow = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
-      double* fr = a.F + ((size_t)b * a.out_rows + orow) * 3;
-      fr[1] = f2;
-      fr[2] = f3;
+  OpTab tab;
+  tab.code = (const int*)(smem + o.opc);
+  tab.arg = (const int4*)(smem + o.opa);
+  tab.k = (const double2*)(smem + o.opk);
+  tab.col = (const int*)(smem + o.ocol);
+  tab.pool = (const int*)(smem + o.pool);
+  tab.C = p.C;
+  tab.n_lane = p.C - p.n_sumdiff;
+  tab.tol = p.tol;
+  unsigned opw[OPS_REG];
+  const int kops = min(OPS_REG, (tab.n_lane + 63) >> 6);
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    const int c = lane + 64 * k;
+    opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
+  }
+  // row sources: mode 1 reads the children k_gen wrote (destination rows), mode 0 the input
+  int src_v = 0, dst_v = 0;
+  if (lane < nrw) {
+    const int i = rc.i0 + wave + 4 * lane;
+    dst_v = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
+    src_v = a.mode == 1 ? dst_v : i;
+  }
+  const double* gsrc = a.mode == 1 ? a.genes_out + (size_t)b * a.out_rows * V
+                                   : a.genes_in + (size_t)b * a.in_rows * V;
+  auto load_row = [&](int k, double* x) {
+    const double* gr = gsrc + (size_t)rdl(src_v, k) * V;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (lane + 64 * t < V) x[t] = gr[lane + 64 * t];
+  };
+  double xn[NT];
+  if (nrw > 0) load_row(0, xn);
+  for (int k = 0; k < nrw; ++k) {
+    double x[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) x[t] = xn[t];
+    if (k + 1 < nrw) load_row(k + 1, xn);
+    const int i = rc.i0 + wave + 4 * k;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (lane + 64 * t < V) {
+        if (IDENT)
+          xrow[(ginf[t] >> 17) & 0x7FFF] = x[t];
+        else
+          scatter_gene(p, xrow, ginf[t], x[t]);
+      }
     }
-    if (hrow) {
-      hrow[1] = f2;
-      hrow[2] = f3;
+    wave_sync();
+    double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+    double* hrow =
+        a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
+    const double f3 = constraints_regs<FULL>(tab, opw, kops, xrow, lane, grow,
+                                             (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
+    if (lane == 0) {
+      if (a.F) a.F[((size_t)b * a.out_rows + rdl(dst_v, k)) * 3 + 2] = f3;
+      if (hrow) hrow[2] = f3;
     }
+    wave_sync();  // the next row's scatter overwrites xrow
   }
 }
 
@@ -650,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_constraints(int slot, int n,
   double* xrow = (double*)smem + (size_t)wave * p.D;
   for (int f = lane; f < p.D; f += 64) xrow[f] = x[(size_t)r * p.D + f];
   wave_sync();
-  constraints_row<FULL>(p, xrow, lane, G + (size_t)r * p.C, nullptr, false);
+  constraints_row<FULL>(global_tab(p), xrow, lane, G + (size_t)r * p.C, nullptr, false);
 }
 
 // Per-state constants: one workgroup per state.
@@ -658,8 +1094,7 @@ __global__ __launch_bounds__(256) void k_setup_states(int slot,
                                                       const double* x_init, const double* xl,
                                                       const double* xu, const float* W1full,
                                                       const float* b1, double* gl, double* gu,
-                                                      double* enc_scale, double* enc_min,
-                                                      double* x0_mm, float* bias1,
+                                                      unsigned char* sblob, float* bias1,
                                                       double* genes0) {
   const DProblem& p = c_rows[slot].p;
   const int b = blockIdx.x;
@@ -696,6 +1131,17 @@ __global__ __launch_bounds__(256) void k_setup_states(int slot,
     gu[(size_t)b * p.V + g] = u;
     genes0[(size_t)b * p.V + g] = x0;
   }
+  const VaryOff vo = vary_offsets(p);
+  double* s_es = (double*)(sblob + (size_t)b * vo.sb + vo.es);
+  double* s_em = (double*)(sblob + (size_t)b * vo.sb + vo.em);
+  double* s_x0 = (double*)(sblob + (size_t)b * vo.sb + vo.x0);
+  double* s_xi = (double*)(sblob + (size_t)b * vo.sb + vo.xi);
+  for (int f = tid; f < p.D; f += blockDim.x) s_xi[f] = xi[f];
+  for (int j = p.Dm + tid; j < p.Dm4; j += blockDim.x) {
+    s_es[j] = 0.0;
+    s_em[j] = 0.0;
+    s_x0[j] = 0.0;
+  }
   for (int j = tid; j < p.Dm; j += blockDim.x) {
     const int f = p.mut_feat[j];
     const double a0 = lo[f], a1 = hi[f];
@@ -705,9 +1151,9 @@ __global__ __launch_bounds__(256) void k_setup_states(int slot,
     if (rng == 0.0) rng = 1.0;
     const double sc = 1.0 / rng;
     const double mi = 0.0 - mn * sc;
-    enc_scale[(size_t)b * p.Dm + j] = sc;
-    enc_min[(size_t)b * p.Dm + j] = mi;
-    x0_mm[(size_t)b * p.Dm + j] = xi[f] * sc + mi;
+    s_es[j] = sc;
+    s_em[j] = mi;
+    s_x0[j] = xi[f] * sc + mi;
   }
   // layer-1 bias fold over the immutable features (fp32, Keras casts inputs to float32)
   const int H1 = p.dims[1];
@@ -734,7 +1180,6 @@ static void configure_lds_once() {
   const int lim = 160 * 1024;
   const void* fns[] = {(const void*)k_mlp<1>,          (const void*)k_mlp<2>,
                        (const void*)k_mlp<4>,          (const void*)k_mlp<8>,
-                       (const void*)k_vary<false>,     (const void*)k_vary<true>,
                        (const void*)k_predict<1>,      (const void*)k_predict<2>,
                        (const void*)k_predict<4>,      (const void*)k_predict<8>,
                        (const void*)k_constraints<false>, (const void*)k_constraints<true>};
@@ -744,17 +1189,106 @@ static void configure_lds_once() {
   done = true;
 }
 
+template <class K>
+static void allow_lds(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  (void)hipGetLastError();
+}
+
+// Rows per k_gen / k_cons workgroup: chunks of at most 64 rows of one state, balanced.
+static int vary_rows_per_wg(int n) {
+  const int nchunk = (n + 63) / 64;
+  return (n + nchunk - 1) / nchunk;
+}
+
+static int vary_nt(const DProblem& p) {
+  const int m = p.V > p.Dm4 ? p.V : p.Dm4;
+  const int nt = (m + 63) / 64;
+  return nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : nt <= 8 ? 8 : 16;
+}
+
+template <bool IDENT, int NT>
+static hipError_t gen_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_gen<IDENT, NT>);
+    configured = true;
+  }
+  hipLaunchKernelGGL((k_gen<IDENT, NT>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  return hipGetLastError();
+}
+
+template <bool FULL, bool IDENT, int NT>
+static hipError_t cons_go(dim3 grid, size_t lds, hipStream_t s, int slot, int h0, int rw) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_cons<FULL, IDENT, NT>);
+    configured = true;
+  }
+  hipLaunchKernelGGL((k_cons<FULL, IDENT, NT>), grid, dim3(VARY_T), lds, s, slot, h0, rw);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream) {
+  if (a.total <= 0) return hipSuccess;
+  const int B = a.total / a.n;
+  const int rw = vary_rows_per_wg(a.n);
+  const dim3 grid(B * ((a.n + rw - 1) / rw));
+  const int nt = vary_nt(a.p);
+  const bool ident = a.p.ident != 0;
+  const size_t lds = gen_lds(vary_offsets(a.p), gen_regc(a.p, nt), ident, a.do_eval != 0).total;
+#define GEN(I, N) return gen_go<I, N>(grid, lds, stream, slot, gen, hist_row0, rw)
+  if (ident) {
+    if (nt == 1) GEN(true, 1);
+    if (nt == 2) GEN(true, 2);
+    if (nt == 4) GEN(true, 4);
+    if (nt == 8) GEN(true, 8);
+    GEN(true, 16);
+  }
+  if (nt == 1) GEN(false, 1);
+  if (nt == 2) GEN(false, 2);
+  if (nt == 4) GEN(false, 4);
+  if (nt == 8) GEN(false, 8);
+  GEN(false, 16);
+#undef GEN
+}
+
+hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  if (a.total <= 0 || !a.do_eval) return hipSuccess;
+  const int B = a.total / a.n;
+  const int rw = vary_rows_per_wg(a.n);
+  const dim3 grid(B * ((a.n + rw - 1) / rw));
+  const int nt = vary_nt(a.p);
+  const size_t lds = cons_lds_total(vary_offsets(a.p));
+#define CONS(F, I, N) return cons_go<F, I, N>(grid, lds, stream, slot, hist_row0, rw)
+  if (a.p.full_ops) {  // LCLD programs: one-hot genes, few genes
+    if (nt == 1) CONS(true, false, 1);
+    if (nt == 2) CONS(true, false, 2);
+    if (nt == 4) CONS(true, false, 4);
+    if (nt == 8) CONS(true, false, 8);
+    CONS(true, false, 16);
+  }
+  if (a.p.ident) {
+    if (nt == 1) CONS(false, true, 1);
+    if (nt == 2) CONS(false, true, 2);
+    if (nt == 4) CONS(false, true, 4);
+    if (nt == 8) CONS(false, true, 8);
+    CONS(false, true, 16);
+  }
+  if (nt == 1) CONS(false, false, 1);
+  if (nt == 2) CONS(false, false, 2);
+  if (nt == 4) CONS(false, false, 4);
+  if (nt == 8) CONS(false, false, 8);
+  CONS(false, false, 16);
+#undef CONS
+}
+
 hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream) {
-  if (a.total <= 0) return hipSuccess;
-  configure_lds_once();
-  const size_t lds = a.do_eval ? (size_t)4 * a.p.D * sizeof(double) : 0;
-  const dim3 grid((a.total + 3) / 4);
-  if (a.p.full_ops)
-    hipLaunchKernelGGL(k_vary<true>, grid, dim3(256), lds, stream, slot, gen, hist_row0);
-  else
-    hipLaunchKernelGGL(k_vary<false>, grid, dim3(256), lds, stream, slot, gen, hist_row0);
-  return hipGetLastError();
+  hipError_t e = launch_gen(a, slot, gen, hist_row0, stream);
+  if (e != hipSuccess) return e;
+  return launch_cons(a, slot, hist_row0, stream);
 }
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
@@ -817,11 +1351,11 @@ hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double*
 
 hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,
                                const double* xu, const float* W1full, const float* b1, double* gl,
-                               double* gu, double* enc_scale, double* enc_min, double* x0_mm,
-                               float* bias1, double* genes0, hipStream_t stream) {
+                               double* gu, unsigned char* sblob, float* bias1, double* genes0,
+                               hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_setup_states, dim3(B), dim3(256), 0, stream, slot, x_init, xl, xu, W1full,
-                     b1, gl, gu, enc_scale, enc_min, x0_mm, bias1, genes0);
+                     b1, gl, gu, sblob, bias1, genes0);
   return hipGetLastError();
 }
 

@@ -23,6 +23,95 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
          (size_t)EVAL_TR * (hmax + 1) * sizeof(float);
 }
 
+// Problem and per-state blobs: HBM images of LDS regions, each region 1-KiB aligned so a
+// workgroup stages the regions it needs with 16-B-per-lane global_load_lds copies.
+//   problem blob  A: constraint program (opa, opk, opc, ocol, pool)       -> k_cons
+//                 B: mutation gap table, gene table, mutable features     -> k_gen
+//                 C: ML scaler at the mutable features (mlS, mlM)         -> k_gen
+//   state blob    X: x_init                                               -> k_cons (k_gen OHE)
+//                 E: encoder MinMax at the mutable features (es, em, x0)  -> k_gen
+struct VaryOff {
+  unsigned opa, opk, opc, ocol, pool, a_end;      // region A at 0
+  unsigned geo, ginfo, mutf, b_at, b_end;         // region B at b_at
+  unsigned mlS, mlM, c_at, vb;                    // region C at c_at; vb = blob bytes
+  unsigned xi, x_end;                             // region X at 0
+  unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
+  unsigned rb;                                    // ML row buffer bytes
+};
+__host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
+  VaryOff o{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const unsigned at = (unsigned)off;
+    off = (off + bytes + 15) & ~(size_t)15;
+    return at;
+  };
+  auto kb = [](size_t x) { return (unsigned)((x + 1023) & ~(size_t)1023); };
+  const size_t C = p.C, Dm4 = p.Dm4;
+  o.opa = take(C * 16);
+  o.opk = take(C * 16);
+  o.opc = take(C * 4);
+  o.ocol = take(C * 4);
+  o.pool = take((size_t)p.n_pool * 4);
+  o.a_end = kb(off);
+  o.b_at = o.a_end;
+  off = o.b_at;
+  o.geo = take((size_t)(p.V + 1) * 4);
+  o.ginfo = take((size_t)((p.V + 3) & ~3) * 4);
+  o.mutf = take(Dm4 * 4);
+  o.b_end = kb(off);
+  o.c_at = o.b_end;
+  off = o.c_at;
+  o.mlS = take(Dm4 * 8);
+  o.mlM = take(Dm4 * 8);
+  o.vb = kb(off);
+  off = 0;
+  o.xi = take((size_t)p.D * 8);
+  o.x_end = kb(off);
+  o.e_at = o.x_end;
+  off = o.e_at;
+  o.es = take(Dm4 * 8);
+  o.em = take(Dm4 * 8);
+  o.x0 = take(Dm4 * 8);
+  o.sb = kb(off);
+  o.rb = (unsigned)(((size_t)p.D * 8 + 15) & ~(size_t)15);
+  return o;
+}
+// k_gen keeps the ML-scaler / encoder coefficients of its genes in registers for IDENT
+// problems with at most 8 genes per lane (no LDS staging of regions C and E then).
+constexpr bool GEN_REGC = false;  // k_gen: coefficients in registers (true) or LDS (false)
+__host__ __device__ inline bool gen_regc(const DProblem& p, int nt) {
+  return GEN_REGC && p.ident && nt <= 8;
+}
+// k_gen LDS: region B [, C, E] [, X + one row per wave for one-hot decoding]
+struct GenLds {
+  unsigned b_at, c_at, e_at, x_at, rows_at, total;
+};
+__host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool ident, bool eval) {
+  GenLds l{};
+  unsigned at = 0;
+  l.b_at = at;
+  at += o.b_end - o.b_at;
+  if (eval && !regc) {
+    l.c_at = at;
+    at += o.vb - o.c_at;
+    l.e_at = at;
+    at += o.sb - o.e_at;
+  }
+  if (eval && !ident) {
+    l.x_at = at;
+    at += o.x_end;
+    l.rows_at = at;
+    at += (VARY_T / 64) * o.rb;
+  }
+  l.total = at;
+  return l;
+}
+// k_cons LDS: region A, region X, one row per wave
+__host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
+  return o.a_end + o.x_end + (VARY_T / 64) * o.rb;
+}
+
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
 
 // Launch-argument ring (constant memory, per device): stage a copy on `stream`, launch with
@@ -31,6 +120,8 @@ hipError_t stage_rows(const RowsArgs& a, hipStream_t stream, int* slot);
 hipError_t release_rows(int slot, hipStream_t stream);
 size_t surv_lds_bytes(int N, int R, int P);
 
+hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream);
+hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream);
 hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream);
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream);
@@ -40,8 +131,8 @@ hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double*
                               double* G, hipStream_t stream);
 hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,
                                const double* xu, const float* W1full, const float* b1, double* gl,
-                               double* gu, double* enc_scale, double* enc_min, double* x0_mm,
-                               float* bias1, double* genes0, hipStream_t stream);
+                               double* gu, unsigned char* sblob, float* bias1, double* genes0,
+                               hipStream_t stream);
 hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream);
 hipError_t launch_select(int B, int P, int O, uint64_t seed, uint32_t stream_key, int gen,
                          const int* pop_slot, int* parents, hipStream_t stream);

@@ -24,7 +24,7 @@ EXPORTED = [
     "mv_last_error", "mv_device_count", "mv_engine_create", "mv_engine_destroy",
     "mv_set_states", "mv_evaluate", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
-    "mv_set_profiling", "mv_get_kernel_times", "mv_mlp_create", "mv_mlp_destroy",
+    "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict",
 ]
 
@@ -89,6 +89,7 @@ def lib():
             "mv_attack_history": [vp, vp, vp],
             "mv_set_profiling": [vp, C.c_int32],
             "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
+            "mv_get_phase_times": [vp, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
         }
@@ -265,8 +266,10 @@ class Engine:
         n = C.c_int32()
         check(lib().mv_get_kernel_times(self._h, C.byref(tv), C.byref(tm), C.byref(ts),
                                         C.byref(n)))
+        ph = (C.c_double * 4)()
+        check(lib().mv_get_phase_times(self._h, ph, C.byref(n)))
         return {"vary_ms": tv.value, "mlp_ms": tm.value, "survive_ms": ts.value,
-                "generations": n.value}
+                "gen_ms": ph[0], "cons_ms": ph[1], "generations": n.value}
 
 
 def survive(F, ref_points, n_survive, mu, seed, gen, ideal, worst, extreme, has_extreme,

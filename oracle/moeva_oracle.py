@@ -808,22 +808,41 @@ def polynomial_mutation(X, xl, xu, eta, do_mutation, rand):
 INT_WIDEN = 0.5 - 1e-16
 
 
+MUT_J = 1024  # Philox indices per offspring row of the mutation stream (csrc MUT_J)
+
+
+def geometric_table(V):
+    """T[k] = floor((1 - 1/V)^k * 2^32), k = 0..V, with the C library pow (math.pow) so
+    the table is bit-identical to the engine's (csrc/api.cpp)."""
+    q = 1.0 - 1.0 / V
+    T = [math.floor(math.pow(q, float(k)) * 4294967296.0) for k in range(V + 1)]
+    return np.minimum(np.array(T, dtype=np.float64), 4294967295.0).astype(np.uint64)
+
+
 def mutation_draws(n_off, V, seed, gen, stream_key=0):
-    """Philox statement: gene g of offspring o mutates iff word[(g%4)] of counter
-    index o*ceil(V/4) + g//4 is < floor(2^32 / V)  (prob = 1/n_var, n_var = V);
-    its uniform is u53 of counter index o*V + g (TAG_MUT_U)."""
-    nq = (V + 3) // 4
+    """Philox statement of ``np.random.random((n, n_var)) < 1/n_var`` (softmax_mutation.py
+    :60-64; prob = 1/n_var, n_var = V) as a Bernoulli process with geometric gaps: the
+    j-th draw of offspring o (counter index o*MUT_J + j, TAG_MUT_MASK) gives the gap
+    = #{k in 1..V : word_x < T[k]} to the next mutated gene; words y, z give its PM
+    uniform u53.  Returns the (n_off, V) mask and the uniforms in row-major mask order."""
+    T = geometric_table(V)[1:]
     sm = px.Stream(seed, gen, px.TAG_MUT_MASK, stream_key)
-    o = np.arange(n_off)[:, None]
-    q = np.arange(nq)[None, :]
-    w = sm.words(o * nq + q)
-    words = np.stack(w, axis=2).reshape(n_off, nq * 4)[:, :V].astype(np.uint64)
-    thr = np.uint64(int(4294967296.0 / V))
-    do = words < thr
-    su = px.Stream(seed, gen, px.TAG_MUT_U, stream_key)
-    oo, gg = np.nonzero(do)
-    a, b, _, _ = su.words(oo * V + gg)
-    return do, px.u53(a, b)
+    do = np.zeros((n_off, V), dtype=bool)
+    u = np.zeros((n_off, V))
+    pos = np.full(n_off, -1, dtype=np.int64)
+    live = np.arange(n_off)
+    j = 0
+    while live.size:
+        w0, w1, w2, _ = sm.words(live * MUT_J + j)
+        gap = (w0.astype(np.uint64)[:, None] < T[None, :]).sum(axis=1)
+        pos[live] += 1 + gap.astype(np.int64)
+        ok = pos[live] < V
+        rows = live[ok]
+        do[rows, pos[rows]] = True
+        u[rows, pos[rows]] = px.u53(w1[ok], w2[ok])
+        live = rows
+        j += 1
+    return do, u[do]
 
 
 def mutation(X, xl, xu, types, seed, gen, eta=20.0, stream_key=0):
