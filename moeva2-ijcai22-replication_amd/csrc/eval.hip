@@ -26,6 +26,7 @@
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
+#include "wave.h"
 
 namespace mv {
 
@@ -77,71 +78,6 @@ hipError_t release_rows(int slot, hipStream_t stream) {
 }
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// Wave-wide reductions without LDS: DPP within rows of 16 lanes (quad_perm xor 1, xor 2,
-// row_half_mirror, row_mirror), then gfx950 permlane16/32 swaps across rows.  Every step
-// combines a lane's value with exactly one partner's (commutative), so all 64 lanes end
-// with the same, deterministic total.
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __double2loint(v), hi = __double2hiint(v);
-  return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
-                          __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
-}
-
-// (value of this lane's row-pair partner half, own half) across 16-lane rows (SWAP=16) or
-// 32-lane halves (SWAP=32): returns {x_first, x_second} with x_first + x_second the pair.
-template <int SWAP>
-__device__ __forceinline__ void swap_f64(double v, double& d0, double& d1) {
-  const int lo = __double2loint(v), hi = __double2hiint(v);
-  if (SWAP == 16) {
-    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    d0 = __hiloint2double(b[0], a[0]);
-    d1 = __hiloint2double(b[1], a[1]);
-  } else {
-    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    d0 = __hiloint2double(b[0], a[0]);
-    d1 = __hiloint2double(b[1], a[1]);
-  }
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-  v = v + dpp_f64<0xB1>(v);
-  v = v + dpp_f64<0x4E>(v);
-  v = v + dpp_f64<0x141>(v);
-  v = v + dpp_f64<0x140>(v);
-  double d0, d1;
-  swap_f64<16>(v, d0, d1);
-  v = d0 + d1;
-  swap_f64<32>(v, d0, d1);
-  return d0 + d1;
-}
-
-__device__ __forceinline__ double nanmax(double a, double b) {
-  if (a != a) return a;
-  if (b != b) return b;
-  return b > a ? b : a;
-}
-
-__device__ __forceinline__ double wave_max(double v) {
-  v = nanmax(v, dpp_f64<0xB1>(v));
-  v = nanmax(v, dpp_f64<0x4E>(v));
-  v = nanmax(v, dpp_f64<0x141>(v));
-  v = nanmax(v, dpp_f64<0x140>(v));
-  double d0, d1;
-  swap_f64<16>(v, d0, d1);
-  v = nanmax(d0, d1);
-  swap_f64<32>(v, d0, d1);
-  return nanmax(d0, d1);
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // numpy float remainder (npy_divmod): result takes the divisor's sign
 __device__ __forceinline__ double py_mod(double a, double b) {

@@ -18,6 +18,7 @@
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
+#include "wave.h"
 
 namespace mv {
 
@@ -27,6 +28,7 @@ struct SurvLds {
   double* F;        // [N*3]
   double* ref;      // [R*3]
   double* U;        // [(R+3)*3] normalised reference directions
+  float4* Uf;       // [R+3] the same in fp32 (association pre-filter)
   double* dist;     // [N]
   double* red;      // [waves*16] reduction scratch
   double* scal;     // [32] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9)
@@ -50,7 +52,7 @@ struct SurvLds {
   int* cand;        // [R+3]
   int* ckey;        // [R+3]
   int* iscal;       // [16]
-  unsigned long long* sortk;  // [pow2 >= max(N, n_perm_slots)] bitonic sort keys
+  unsigned long long* sortk;  // [max(N, n_perm_slots)] sort keys
   int* perm;        // [n_perm_slots]
   unsigned long long* dmin;  // [R+3]
   int* lround;      // [2N+2] round index of each level
@@ -66,9 +68,9 @@ __host__ __device__ __forceinline__ int pow2_at_least(int n) {
 
 // Byte offsets of the survival workspace inside the dynamic LDS block.
 struct SurvOff {
-  unsigned F, ref, U, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
-      key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm, dmin,
-      lround, total;
+  unsigned F, ref, U, Uf, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
+      key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm,
+      dmin, lround, total;
 };
 
 __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
@@ -82,6 +84,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(F, (size_t)N * 3 * 8)
   TAKE(ref, (size_t)R * 3 * 8)
   TAKE(U, (size_t)RN * 3 * 8)
+  TAKE(Uf, (size_t)RN * 16)
   TAKE(dist, (size_t)N * 8)
   TAKE(red, (SURV_T / 64) * 16 * 8)
   TAKE(scal, 32 * 8)
@@ -105,7 +108,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(cand, RN * 4)
   TAKE(ckey, RN * 4)
   TAKE(iscal, 16 * 4)
-  TAKE(sortk, (size_t)pow2_at_least(N > Pperm ? N : Pperm) * 8)
+  TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
   TAKE(perm, (size_t)Pperm * 4)
   TAKE(dmin, (size_t)RN * 8)
   TAKE(lround, (size_t)(2 * N + 2) * 4)
@@ -193,12 +196,10 @@ __device__ __forceinline__ int block_scan_excl(int* v, int n, int* wsum) {
 }
 
 __device__ __forceinline__ double wred_min(double v) {
-  for (int o = 32; o > 0; o >>= 1) v = min_prop(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](double a, double b) { return min_prop(a, b); });
 }
 __device__ __forceinline__ double wred_max(double v) {
-  for (int o = 32; o > 0; o >>= 1) v = max_prop(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](double a, double b) { return max_prop(a, b); });
 }
 // LAPACK dgetf2/dgetrs-order 3x3 solve (oracle lu_solve3).  Returns false if singular.
 __device__ bool lu_solve3(double A[3][3], double x[3]) {
@@ -231,27 +232,6 @@ __device__ bool lu_solve3(double A[3][3], double x[3]) {
   return true;
 }
 
-// Ascending bitonic sort of k[0, n2) (n2 a power of two; callers pad with ~0).  Keys are
-// unique composites (order fields << ... | index), so the order is total and deterministic.
-__device__ __forceinline__ void block_sort_u64(unsigned long long* k, int n2) {
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n2; i += SURV_T) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const unsigned long long x = k[i], y = k[j];
-          const bool up = (i & size) == 0;
-          if ((x > y) == up) {
-            k[i] = y;
-            k[j] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // Tournament selection for the next generation (oracle tournament_parents).
 __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
                            const int* map_slot, int* out, unsigned long long* sortk,
@@ -261,24 +241,26 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
   const int n_random = n_m * 4;
   const int n_perms = (n_random + P - 1) / P;
   const int n = n_perms * P;
-  const int n2 = pow2_at_least(n);
   const Rng rng(seed, sk);
   int ib = 1;  // bits of the index field
   while ((1 << ib) < P) ++ib;
   const unsigned long long imask = (1ull << ib) - 1ull;
-  // permutation q = argsort of its P keys (ties by index): sort (q, key, i) composites
-  for (int idx = tid; idx < n2; idx += SURV_T) {
-    unsigned long long v = ~0ull;
-    if (idx < n) {
-      const int q = idx / P, i = idx - q * P;
-      const unsigned key = rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
-      v = ((unsigned long long)q << (32 + ib)) | ((unsigned long long)key << ib) | (unsigned)i;
-    }
-    sortk[idx] = v;
+  // permutation q = argsort of its P keys (ties by index): rank of each (key, i) composite
+  // among the P composites of its own permutation
+  for (int idx = tid; idx < n; idx += SURV_T) {
+    const int q = idx / P, i = idx - q * P;
+    const unsigned key = rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
+    sortk[idx] = ((unsigned long long)key << ib) | (unsigned)i;
   }
   __syncthreads();
-  block_sort_u64(sortk, n2);
-  for (int idx = tid; idx < n; idx += SURV_T) perm[idx] = (int)(sortk[idx] & imask);
+  for (int idx = tid; idx < n; idx += SURV_T) {
+    const int q = idx / P;
+    const unsigned long long kp = sortk[idx];
+    const unsigned long long* kq = sortk + (size_t)q * P;
+    int r = 0;
+    for (int j = 0; j < P; ++j) r += kq[j] < kp ? 1 : 0;
+    perm[q * P + r] = (int)(kp & imask);
+  }
   __syncthreads();
   for (int t = tid; t < 2 * n_m; t += SURV_T) {
     const int a = perm[2 * t], b = perm[2 * t + 1];
@@ -303,6 +285,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   L.F = (double*)(smem + o.F);
   L.ref = (double*)(smem + o.ref);
   L.U = (double*)(smem + o.U);
+  L.Uf = (float4*)(smem + o.Uf);
   L.dist = (double*)(smem + o.dist);
   L.red = (double*)(smem + o.red);
   L.scal = (double*)(smem + o.scal);
@@ -555,14 +538,9 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       }
     }
     for (int i = 0; i < 3; ++i) {
-      for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(bv[i], o, 64);
-        const int oi = __shfl_xor(bi[i], o, 64);
-        if (arg_better(ov, oi, bv[i], bi[i])) {
-          bv[i] = ov;
-          bi[i] = oi;
-        }
-      }
+      wave_argbest(bv[i], bi[i], [](double v, int i1, double w, int i2) {
+        return arg_better(v, i1, w, i2);
+      });
       wf[i] = wred_max(wf[i]);
     }
     __syncthreads();
@@ -669,6 +647,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       }
       const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
       for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
+      L.Uf[r] = make_float4((float)L.U[r * 3], (float)L.U[r * 3 + 1], (float)L.U[r * 3 + 2], 0.f);
     }
     if (tid == 0) L.iscal[15] = 0;
     __syncthreads();
@@ -686,38 +665,64 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
-      // argmin over squared distances (first index on exact ties, like np.argmin).  Two
-      // DIFFERENT squared distances can share a sqrt: flag when a distance differs from the
-      // running best by at most 1e-15 relative (or is NaN); the exact np.argmin over the
-      // sqrt'ed values below then decides.  Branchless, 4 directions per step.
-      double best = __builtin_inf();
-      int bj = 0;
-      bool flag = false;
-      const double c = 1.0 + 1e-15;
-      auto d2_of = [&](int j) {
-        const double* u = &L.U[j * 3];
-        const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
-        const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
-        return (e0 * e0 + e1 * e1) + e2 * e2;
+      // fp32 pre-filter of the squared perpendicular distances.  Its error is below
+      // 4e-6 |N|^2, so only directions whose fp32 value is within tol = 3e-5 (|N|^2 + best)
+      // of the fp32 minimum can hold the fp64 minimum: those few get the exact fp64
+      // distance and np.argmin's order (first index among equal sqrt'ed distances).  A NaN
+      // or overflow sends the individual to the full exact pass below.
+      const float n0 = (float)Nn[0], n1 = (float)Nn[1], n2 = (float)Nn[2];
+      auto d2f = [&](int j) {
+        const float4 u = L.Uf[j];
+        const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
+        const float e0 = fmaf(sp, u.x, -n0), e1 = fmaf(sp, u.y, -n1), e2 = fmaf(sp, u.z, -n2);
+        return fmaf(e0, e0, fmaf(e1, e1, e2 * e2));
       };
-      auto take = [&](double d2, int j) {
-        flag = flag | (d2 != d2) | ((d2 != best) & (d2 <= best * c) & (best <= d2 * c));
-        const bool lt = d2 < best;
-        best = lt ? d2 : best;
-        bj = lt ? j : bj;
-      };
-      int j0 = 0;
-      for (; j0 + 4 <= RN; j0 += 4) {
-        const double d0 = d2_of(j0), d1 = d2_of(j0 + 1), d2 = d2_of(j0 + 2), d3 = d2_of(j0 + 3);
-        take(d0, j0);
-        take(d1, j0 + 1);
-        take(d2, j0 + 2);
-        take(d3, j0 + 3);
+      if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
+          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0
+        L.niche[p] = 0;
+        L.dist[p] = 0.0;
+        continue;
       }
-      for (; j0 < RN; ++j0) take(d2_of(j0), j0);
-      L.niche[p] = bj;
-      L.dist[p] = sqrt(best);
-      if (flag) L.key[atomicAdd(&L.iscal[15], 1)] = p;
+      float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;  // 4 independent chains
+      int j = 0;
+      for (; j + 4 <= RN; j += 4) {
+        b0 = fminf(b0, d2f(j));
+        b1 = fminf(b1, d2f(j + 1));
+        b2 = fminf(b2, d2f(j + 2));
+        b3 = fminf(b3, d2f(j + 3));
+      }
+      for (; j < RN; ++j) b0 = fminf(b0, d2f(j));
+      const float best = fminf(fminf(b0, b1), fminf(b2, b3));
+      const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
+      const float lim = best + 3e-5f * (nn + best);
+      if (lim < __builtin_inff()) {  // false on NaN / inf
+        double bd = __builtin_inf();
+        int bj = 0;
+        auto cand = [&](int j) {  // exact fp64 distance, np.argmin order
+          const double* u = &L.U[j * 3];
+          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+          if (arg_better(dd, j, bd, bj)) {
+            bd = dd;
+            bj = j;
+          }
+        };
+        int j = 0;
+        for (; j + 4 <= RN; j += 4) {  // rare beyond the minimum itself
+          const float d0 = d2f(j), d1 = d2f(j + 1), d2 = d2f(j + 2), d3 = d2f(j + 3);
+          if (d0 <= lim) cand(j);
+          if (d1 <= lim) cand(j + 1);
+          if (d2 <= lim) cand(j + 2);
+          if (d3 <= lim) cand(j + 3);
+        }
+        for (; j < RN; ++j)
+          if (d2f(j) <= lim) cand(j);
+        L.niche[p] = bj;
+        L.dist[p] = bd;
+      } else {
+        L.key[atomicAdd(&L.iscal[15], 1)] = p;
+      }
     }
     __syncthreads();
     PHASE(10)
@@ -778,23 +783,19 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       bestkr[n] = INT_MAX;
     }
     for (int l = tid; l < nlev; l += SURV_T) L.lround[l] = 0;
-    const int n2 = pow2_at_least(Lc);
     unsigned long long* sk = L.sortk;
     for (int p = tid; p < until; p += SURV_T) atomicAdd(&cnt[L.niche[p]], 1);
-    // member order inside each niche: ascending (niche, member key, position)
-    for (int p = tid; p < n2; p += SURV_T) {
-      unsigned long long v = ~0ull;
-      if (p < Lc) {
-        const unsigned key = rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
-        atomicAdd(&mcnt[nich[p]], 1);
-        v = ((unsigned long long)nich[p] << 41) | ((unsigned long long)key << 9) | (unsigned)p;
-      }
-      sk[p] = v;
+    // member order inside each niche: ascending (niche, member key, position); grank = rank
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const unsigned key = rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
+      atomicAdd(&mcnt[nich[p]], 1);
+      sk[p] = ((unsigned long long)nich[p] << 41) | ((unsigned long long)key << 9) | (unsigned)p;
     }
     __syncthreads();
-    block_sort_u64(sk, n2);
-    for (int r = tid; r < Lc; r += SURV_T) {
-      const int p = (int)(sk[r] & 511ull);
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const unsigned long long kp = sk[p];
+      int r = 0;
+      for (int q = 0; q < Lc; ++q) r += sk[q] < kp ? 1 : 0;
       const int np_ = nich[p];
       grank[p] = r;
       if (cnt[np_] == 0)
@@ -821,21 +822,21 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     __syncthreads();
     block_scan_excl(L.lround, nlev, wsum);  // rounds before each level
     // output order: ascending (level, round key of the niche, niche); a niche picks at most
-    // once per level, so the sorted index is the pick's position among the remaining slots
-    for (int p = tid; p < n2; p += SURV_T) {
-      unsigned long long v = ~0ull;
-      if (p < Lc) {
-        const int l = lev[p];
-        const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
-                                     TAG_NICHE_PERM).x;
-        v = ((unsigned long long)l << 51) | ((unsigned long long)kr << 19) |
-            ((unsigned long long)nich[p] << 9) | (unsigned)p;
-      }
-      sk[p] = v;
+    // once per level, so a pick's rank is its position among the remaining slots
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int l = lev[p];
+      const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
+                                   TAG_NICHE_PERM).x;
+      sk[p] = ((unsigned long long)l << 51) | ((unsigned long long)kr << 19) |
+              ((unsigned long long)nich[p] << 9) | (unsigned)p;
     }
     __syncthreads();
-    block_sort_u64(sk, n2);
-    for (int r = tid; r < n_rem; r += SURV_T) L.surv[until + r] = fs + (int)(sk[r] & 511ull);
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const unsigned long long kp = sk[p];
+      int r = 0;
+      for (int q = 0; q < Lc; ++q) r += sk[q] < kp ? 1 : 0;
+      if (r < n_rem) L.surv[until + r] = fs + p;
+    }
     for (int p = tid; p < until; p += SURV_T) L.surv[p] = p;
     n_out = a.n_survive;
   } else {

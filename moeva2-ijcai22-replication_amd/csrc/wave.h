@@ -1,0 +1,137 @@
+// Wave-level building blocks shared by the kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mv {
+
+// Wave-wide reductions without LDS: DPP within rows of 16 lanes (quad_perm xor 1, xor 2,
+// row_half_mirror, row_mirror), then gfx950 permlane16/32 swaps across rows.  Every step
+// combines a lane's value with exactly one partner's (commutative), so all 64 lanes end
+// with the same, deterministic total.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false),
+                          __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false));
+}
+
+// (value of this lane's row-pair partner half, own half) across 16-lane rows (SWAP=16) or
+// 32-lane halves (SWAP=32): returns {x_first, x_second} with x_first + x_second the pair.
+template <int SWAP>
+__device__ __forceinline__ void swap_f64(double v, double& d0, double& d1) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  if (SWAP == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    d0 = __hiloint2double(b[0], a[0]);
+    d1 = __hiloint2double(b[1], a[1]);
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    d0 = __hiloint2double(b[0], a[0]);
+    d1 = __hiloint2double(b[1], a[1]);
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  v = v + dpp_f64<0xB1>(v);
+  v = v + dpp_f64<0x4E>(v);
+  v = v + dpp_f64<0x141>(v);
+  v = v + dpp_f64<0x140>(v);
+  double d0, d1;
+  swap_f64<16>(v, d0, d1);
+  v = d0 + d1;
+  swap_f64<32>(v, d0, d1);
+  return d0 + d1;
+}
+
+__device__ __forceinline__ double nanmax(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  return b > a ? b : a;
+}
+
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+  v = op(v, dpp_f64<0xB1>(v));
+  v = op(v, dpp_f64<0x4E>(v));
+  v = op(v, dpp_f64<0x141>(v));
+  v = op(v, dpp_f64<0x140>(v));
+  double d0, d1;
+  swap_f64<16>(v, d0, d1);
+  v = op(d0, d1);
+  swap_f64<32>(v, d0, d1);
+  return op(d0, d1);
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+template <int SWAP>
+__device__ __forceinline__ void swap_i32(int v, int& d0, int& d1) {
+  if (SWAP == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    d0 = a[0];
+    d1 = a[1];
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    d0 = a[0];
+    d1 = a[1];
+  }
+}
+
+// (value, index) reduction: better(v, i, bv, bi) must be a strict total order, so every lane
+// ends with the same winner.
+template <class Better>
+__device__ __forceinline__ void wave_argbest(double& v, int& i, Better better) {
+#define MV_ARG_STEP(CTRL)                                   \
+  {                                                         \
+    const double ov = dpp_f64<CTRL>(v);                     \
+    const int oi = dpp_i32<CTRL>(i);                        \
+    if (better(ov, oi, v, i)) {                             \
+      v = ov;                                               \
+      i = oi;                                               \
+    }                                                       \
+  }
+  MV_ARG_STEP(0xB1)
+  MV_ARG_STEP(0x4E)
+  MV_ARG_STEP(0x141)
+  MV_ARG_STEP(0x140)
+#undef MV_ARG_STEP
+  double d0, d1;
+  int i0, i1;
+  swap_f64<16>(v, d0, d1);
+  swap_i32<16>(i, i0, i1);
+  if (better(d1, i1, d0, i0)) {
+    d0 = d1;
+    i0 = i1;
+  }
+  swap_f64<32>(d0, v, d1);
+  swap_i32<32>(i0, i, i1);
+  if (better(d1, i1, v, i)) {
+    v = d1;
+    i = i1;
+  }
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+  v = nanmax(v, dpp_f64<0xB1>(v));
+  v = nanmax(v, dpp_f64<0x4E>(v));
+  v = nanmax(v, dpp_f64<0x141>(v));
+  v = nanmax(v, dpp_f64<0x140>(v));
+  double d0, d1;
+  swap_f64<16>(v, d0, d1);
+  v = nanmax(d0, d1);
+  swap_f64<32>(v, d0, d1);
+  return nanmax(d0, d1);
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+}  // namespace mv
