@@ -99,6 +99,20 @@ struct mv_engine {
     if (e == hipSuccess) xml_cap = need;
     return e;
   }
+  // state-group streams (index 0 = the caller's stream, not owned)
+  hipStream_t streams[MAX_GROUPS] = {};
+  hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_join[MAX_GROUPS] = {};
+  hipError_t ensure_streams(int n) {
+    hipError_t err = hipSuccess;
+    if (!ev_fork) err = hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming);
+    for (int q = 1; q < n && err == hipSuccess; ++q) {
+      if (!streams[q]) err = hipStreamCreateWithFlags(&streams[q], hipStreamNonBlocking);
+      if (err == hipSuccess && !ev_join[q])
+        err = hipEventCreateWithFlags(&ev_join[q], hipEventDisableTiming);
+    }
+    return err;
+  }
   // profiling
   bool profiling = false;
   std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
@@ -123,6 +137,11 @@ struct mv_engine {
     for (auto e : ev_var) (void)hipEventDestroy(e);
     for (auto e : ev_mlp) (void)hipEventDestroy(e);
     for (auto e : ev_cons) (void)hipEventDestroy(e);
+    for (int q = 1; q < MAX_GROUPS; ++q) {
+      if (streams[q]) (void)hipStreamDestroy(streams[q]);
+      if (ev_join[q]) (void)hipEventDestroy(ev_join[q]);
+    }
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
@@ -165,7 +184,7 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   p.D = D;
   p.V = V;
   p.Dm = Dm;
-  p.Dm4 = (Dm + 3) & ~3;
+  p.Dm4 = (Dm + 15) & ~15;  // mutable features padded to a 16-k MFMA group
   p.C = C;
   p.n_ohe = pd->n_ohe;
   std::vector<int> sub(V);
@@ -210,7 +229,7 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   K((double**)&p.ml_scale, mls.data(), D);
   K((double**)&p.ml_min, mlm.data(), D);
   {
-    const int Dm4 = (Dm + 3) & ~3;
+    const int Dm4 = p.Dm4;
     std::vector<double> ms(Dm4, 0.0), mm(Dm4, 0.0);
     for (int j = 0; j < Dm; ++j) {
       ms[j] = mls[pd->mut_feats[j]];
@@ -308,6 +327,18 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     for (int l = 1; l < md->n_layers; ++l) {
       K((float**)&p.W[l], md->W[l], (size_t)md->dims[l] * md->dims[l + 1]);
       K((float**)&p.bias[l], md->b[l], md->dims[l + 1]);
+    }
+    // k_mlp2 packing of the hidden layers: Wp[kg][n][16] = W[16 kg + i][n] (zero padded)
+    p.mlp2 = 1;
+    for (int l = 1; l < md->n_layers; ++l) p.mlp2 &= md->dims[l] % 16 == 0 && md->dims[l] <= 128;
+    for (int l = 0; l + 1 < md->n_layers && p.mlp2; ++l) {
+      const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
+      const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major
+      std::vector<float> wp((size_t)Kl * Nl, 0.f);
+      for (int k = 0; k < Kl; ++k)
+        for (int n = 0; n < Nl; ++n)
+          wp[((size_t)(k / 16) * Nl + n) * 16 + (k % 16)] = src[(size_t)k * Nl + n];
+      K((float**)&p.Wp[l], wp.data(), wp.size());
     }
   } else {
     p.n_layers = 0;
@@ -568,10 +599,64 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   hipLaunchKernelGGL(k_fill_i, dim3(64), dim3(256), 0, stream, e->has_ext, (size_t)B, 0);
   HIPCHK(hipGetLastError());
   HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
+  // Initial states are independent: split them into state groups, each running its own
+  // generation chain on its own stream, so one group's latency-bound survival overlaps the
+  // other groups' throughput-bound kernels.  Results do not depend on the grouping (every
+  // draw is keyed by the row inside its state).  Profiling runs use one group so the
+  // per-kernel event times are those of the kernels alone.
+  int ngrp = B / 64;  // about 100 states per group at the botnet size
+  if (const char* g = std::getenv("MV_GROUPS")) ngrp = std::atoi(g);
+  if (e->profiling) ngrp = 1;
+  ngrp = ngrp < 1 ? 1 : (ngrp > MAX_GROUPS ? MAX_GROUPS : (ngrp > B ? B : ngrp));
+  HIPCHK(e->ensure_streams(ngrp));
+  hipStream_t gs[MAX_GROUPS];
+  int gb0[MAX_GROUPS + 1];
+  for (int q = 0; q <= ngrp; ++q) gb0[q] = (int)((long long)B * q / ngrp);
+  gs[0] = stream;
+  if (ngrp > 1) HIPCHK(hipEventRecord(e->ev_fork, stream));
+  for (int q = 1; q < ngrp; ++q) {
+    gs[q] = e->streams[q];
+    HIPCHK(hipStreamWaitEvent(gs[q], e->ev_fork, 0));
+  }
+  const int H1 = e->H1, D = e->p.D;
+  const unsigned sbb = vary_offsets(e->p).sb;
+  const size_t Dm4 = e->p.Dm4;
+  auto group_rows = [&](RowsArgs r, int q, int n_per_state) {
+    const size_t b0 = gb0[q];
+    r.s.B = gb0[q + 1] - gb0[q];
+    r.s.x_init += b0 * D;
+    r.s.gl += b0 * V;
+    r.s.gu += b0 * V;
+    r.s.sblob += b0 * sbb;
+    r.s.bias1 += b0 * H1;
+    r.s.min_class += b0;
+    r.total = r.s.B * n_per_state;
+    if (r.genes_in) r.genes_in += b0 * r.in_rows * V;
+    if (r.genes_out) r.genes_out += b0 * r.out_rows * V;
+    if (r.parents) r.parents += b0 * O;
+    if (r.out_map) r.out_map += b0 * r.n;
+    if (r.F) r.F += b0 * r.out_rows * 3;
+    if (r.hist) r.hist += b0 * (size_t)r.hist_rows * r.hist_w;
+    r.xml += b0 * (size_t)r.n * Dm4;
+    return r;
+  };
+  auto group_surv = [&](SurvArgs s, int q) {
+    const size_t b0 = gb0[q];
+    s.F += b0 * S * 3;
+    s.pop_slot += b0 * P;
+    s.free_slot += b0 * O;
+    s.pop_slot_out += b0 * P;
+    s.ideal += b0 * 3;
+    s.worst += b0 * 3;
+    s.extreme += b0 * 9;
+    s.has_extreme += b0;
+    if (s.parents_out) s.parents_out += b0 * O;
+    if (s.phase) s.phase += b0 * 16;
+    return s;
+  };
   // initial population evaluation (pymoo _initialize)
   RowsArgs ev = base_rows(e);
   ev.n = P;
-  ev.total = B * P;
   ev.mode = 0;
   ev.genes_in = e->pool;
   ev.in_rows = S;
@@ -582,10 +667,6 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   ev.hist_w = hist_w;
   HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
   ev.xml = e->xml;
-  int slot_ev = 0;
-  HIPCHK(stage_rows(ev, stream, &slot_ev));
-  HIPCHK(launch_rows(ev, slot_ev, 0, 0, stream));
-  HIPCHK(release_rows(slot_ev, stream));
   SurvArgs sa{};
   sa.n_survive = P;
   sa.P = P;
@@ -616,7 +697,14 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.gen = 0;
   sa.parents_out = G > 1 ? e->parents : nullptr;
   sa.sel_gen = 1;
-  HIPCHK(launch_survive(sa, B, stream));
+  for (int q = 0; q < ngrp; ++q) {
+    int slot_ev = 0;
+    const RowsArgs evq = group_rows(ev, q, P);
+    HIPCHK(stage_rows(evq, gs[q], &slot_ev));
+    HIPCHK(launch_rows(evq, slot_ev, 0, 0, gs[q]));
+    HIPCHK(release_rows(slot_ev, gs[q]));
+    HIPCHK(launch_survive(group_surv(sa, q), gb0[q + 1] - gb0[q], gs[q]));
+  }
   if (e->profiling) {
     if (ensure_events(e->ev_var, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_mlp, (size_t)G) != MV_OK) return MV_ERR_HIP;
@@ -627,7 +715,6 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   e->n_surv_rec = 0;
   RowsArgs va = base_rows(e);
   va.n = O;
-  va.total = B * O;
   va.mode = 1;
   va.genes_in = e->pool;
   va.in_rows = S;
@@ -641,26 +728,38 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_w = hist_w;
   va.seed = prm->seed;
   va.xml = e->xml;
-  int slot_va = 0;
-  HIPCHK(stage_rows(va, stream, &slot_va));
+  int slot_va[MAX_GROUPS];
+  RowsArgs vq[MAX_GROUPS];
+  for (int q = 0; q < ngrp; ++q) {
+    vq[q] = group_rows(va, q, O);
+    HIPCHK(stage_rows(vq[q], gs[q], &slot_va[q]));
+  }
   sa.N = P + O;
   for (int g = 1; g < G; ++g) {
     const int hist_row0 = P + (g - 1) * O;
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], stream));
-    HIPCHK(launch_gen(va, slot_va, g, hist_row0, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], stream));
-    HIPCHK(launch_cons(va, slot_va, hist_row0, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], stream));
-    HIPCHK(launch_mlp(va, slot_va, hist_row0, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], stream));
     sa.gen = g;
     sa.parents_out = g + 1 < G ? e->parents : nullptr;
     sa.sel_gen = g + 1;
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec], stream));
-    HIPCHK(launch_survive(sa, B, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec++ + 1], stream));
+    for (int q = 0; q < ngrp; ++q) {
+      hipStream_t st = gs[q];
+      const bool prof = e->profiling && q == 0;
+      if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
+      HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+      HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
+      HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec], st));
+      HIPCHK(launch_survive(group_surv(sa, q), gb0[q + 1] - gb0[q], st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec++ + 1], st));
+    }
   }
-  HIPCHK(release_rows(slot_va, stream));
+  for (int q = 0; q < ngrp; ++q) HIPCHK(release_rows(slot_va[q], gs[q]));
+  for (int q = 1; q < ngrp; ++q) {  // join: the caller's stream waits for every group
+    HIPCHK(hipEventRecord(e->ev_join[q], gs[q]));
+    HIPCHK(hipStreamWaitEvent(stream, e->ev_join[q], 0));
+  }
   return MV_OK;
 }
 

@@ -18,17 +18,17 @@ namespace mv {
 constexpr int MAX_LAYERS = 6;
 constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
 constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
-constexpr int VARY_T = 256;      // threads per k_vary workgroup (4 waves, one row buffer each)
-constexpr int VARY_MAX_ROWS = 256;  // rows per k_vary workgroup (<= 64 per wave)
+constexpr int VARY_T = 256;      // threads per k_gen / k_cons workgroup (4 waves)
 constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
 constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS
 constexpr int SURV_RMAX = 640;   // reference points
 constexpr int ARG_SLOTS = 32;    // constant-memory launch-argument slots per device
+constexpr int MAX_GROUPS = 4;    // state groups (streams) of one attack
 constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound widening
 
 struct DProblem {
-  int D, V, Dm, Dm4, C, n_ohe;
+  int D, V, Dm, Dm4, C, n_ohe;  // Dm4: mutable features padded to a multiple of 16
   int n_sub[2];           // crossover subsets: 0 real, 1 int (OHE genes are int)
   const int* gene_kind;   // [V]
   const int* gene_feat;   // [V]
@@ -62,6 +62,11 @@ struct DProblem {
   int dims[MAX_LAYERS + 1];
   const float* W[MAX_LAYERS];     // W[0]: mutable rows only, [Dm4][dims[1]] zero-padded
   const float* bias[MAX_LAYERS];  // bias[0] unused at run time (folded per state)
+  // k_mlp2 weights: per hidden layer l, [K_l/16][N_l][16] (16 consecutive k of one output
+  // column contiguous; K_0 = Dm4, K_l = dims[l]), so one dwordx4 load is a lane's B operand
+  // for four 16x16x4 MFMA k-steps
+  const float* Wp[MAX_LAYERS];
+  int mlp2;               // hidden widths fit k_mlp2 (multiples of 16, <= 128)
 };
 
 struct DStates {

@@ -21,6 +21,7 @@
 // pointers they hold lose their address space (every access became a flat op); pointers
 // loaded from the constant address space are known to be global.  Only the
 // per-generation scalars (slot, gen, first history row) are passed by value.
+#include <cstdlib>
 #include <mutex>
 
 #include "engine.h"
@@ -962,6 +963,211 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_mlp2: the Dense-ReLU chain + final Dense/softmax over 64-row tiles (persistent
+// workgroups), for hidden widths that are multiples of 16 and at most 128.
+//
+// Layer l multiplies the tile's [64][K_l] activations by W_l on v_mfma_f32_16x16x4_f32
+// (exact fp32 products).  K is walked in groups of 16: lane (il, ka) of a wave holds
+// k = 16 kg + 4 ka + s for the group's four MFMA k-steps s, so its A operands are one
+// ds_read_b128 of a row and its B operands one dwordx4 of the packed weights
+// Wp_l[kg][n][16].  Wave w owns output column tiles w, w + 4, ... and all four 16-row
+// tiles, so each B load feeds four MFMAs.  Layer 0 streams the fp32 ML rows written by
+// k_gen through a double-buffered LDS chunk of 64 k (register staged); hidden outputs go to
+// an LDS ping-pong; the immutable features' contribution to layer 0 is the per-state bias
+// bias1 (k_setup_states).  The last Dense + softmax is a dot product per row on the VALU.
+constexpr int M2_ROWS = 64;
+constexpr int M2_ALD = 68;  // layer-0 chunk row stride (floats)
+
+__host__ __device__ inline int mlp2_hmax(const DProblem& p) {
+  int h = 16;
+  for (int l = 1; l < p.n_layers; ++l) h = p.dims[l] > h ? p.dims[l] : h;
+  return h;
+}
+__host__ __device__ inline size_t mlp2_head(const DProblem& p) {
+  const int nl = p.n_layers;
+  return 256 + (((size_t)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~(size_t)15);
+}
+__host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
+  const size_t hld = mlp2_hmax(p) + 4;
+  return mlp2_head(p) + (size_t)2 * M2_ROWS * M2_ALD * 4 + 2 * M2_ROWS * hld * 4;
+}
+
+template <int CJ>
+__device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
+                                           const float* __restrict__ Wp, int nkg, int N,
+                                           floatx4 (&acc)[CJ][4], int wave, int il, int ka) {
+  const int nct = N >> 4;
+  auto load_b = [&](int kg, float4 (&bf)[CJ]) {
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) {
+      const int ct = wave + 4 * cj;
+      bf[cj] = (ct < nct && kg < nkg)
+                   ? *(const float4*)(Wp + ((size_t)kg * N + ct * 16 + il) * 16 + 4 * ka)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto load_a = [&](int kg, float4 (&af)[4]) {
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+      af[rt] = *(const float4*)(A + (rt * 16 + il) * lda + kg * 16 + 4 * ka);
+  };
+  float4 bf[CJ], af[4];
+  load_b(0, bf);
+  load_a(0, af);
+  for (int kg = 0; kg < nkg; ++kg) {
+    float4 bn[CJ], an[4];
+    load_b(kg + 1, bn);  // next group's weights (L2) while this group's MFMAs run
+    if (kg + 1 < nkg) load_a(kg + 1, an);
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) {
+      if (wave + 4 * cj < nct) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].x, bf[cj].x, acc[cj][rt], 0, 0, 0);
+          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].y, bf[cj].y, acc[cj][rt], 0, 0, 0);
+          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].z, bf[cj].z, acc[cj][rt], 0, 0, 0);
+          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].w, bf[cj].w, acc[cj][rt], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
+    if (kg + 1 < nkg) {
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) af[rt] = an[rt];
+    }
+  }
+}
+
+template <int CJ>
+__global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int il = lane & 15, ka = lane >> 4;
+  const int nl = p.n_layers;
+  const int K0 = p.Dm4, N0 = p.dims[1];
+  const int hld = mlp2_hmax(p) + 4;
+  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
+  int* rowst = (int*)smem;
+  float* wl = (float*)(smem + 256);
+  float* bl = wl + Klast * nout;
+  float* A0 = (float*)(smem + mlp2_head(p));
+  float* H = A0 + 2 * M2_ROWS * M2_ALD;
+  for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
+  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
+  const int nkg0 = K0 >> 4;
+  const int nch = (nkg0 + 3) >> 2;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r0 = tile * M2_ROWS;
+    float4 st[4];
+    auto chunk_load = [&](int c) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = tid + 256 * u;
+        const int row = idx >> 4, q = idx & 15;
+        const int k = c * 64 + 4 * q;
+        st[u] = (r0 + row < a.total && k < K0)
+                    ? *(const float4*)(a.xml + (size_t)(r0 + row) * K0 + k)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    auto chunk_store = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = tid + 256 * u;
+        const int row = idx >> 4, q = idx & 15;
+        *(float4*)(A0 + buf * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = st[u];
+      }
+    };
+    chunk_load(0);
+    __syncthreads();  // the previous tile's readers of rowst / A0 / H are done
+    if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
+    chunk_store(0);
+    __syncthreads();
+    floatx4 acc[CJ][4];
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj)
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) chunk_load(c + 1);
+      const int ng = min(4, nkg0 - 4 * c);
+      mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, p.Wp[0] + (size_t)4 * c * N0 * 16,
+                     ng, N0, acc, wave, il, ka);
+      if (c + 1 < nch) chunk_store((c + 1) & 1);
+      __syncthreads();
+    }
+    // hidden layers: layer l writes H[l & 1]
+    for (int l = 0; l + 1 < nl; ++l) {
+      const int N = p.dims[l + 1];
+      if (l > 0) {
+#pragma unroll
+        for (int cj = 0; cj < CJ; ++cj)
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N, acc,
+                       wave, il, ka);
+      }
+      float* out = H + (l & 1) * M2_ROWS * hld;
+#pragma unroll
+      for (int cj = 0; cj < CJ; ++cj) {
+        const int ct = wave + 4 * cj;
+        if (ct < (N >> 4)) {
+          const int col = ct * 16 + il;
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int row = rt * 16 + ka * 4 + j;
+              float bv;
+              if (l == 0) {
+                const int s = rowst[row];
+                bv = a.s.bias1[(size_t)(s < 0 ? 0 : s) * N0 + col];
+              } else {
+                bv = p.bias[l][col];
+              }
+              const float v = acc[cj][rt][j] + bv;
+              out[row * hld + col] = v > 0.f ? v : 0.f;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // final Dense + softmax (classifier.py:23-29) -> f1
+    if (tid < M2_ROWS) {
+      const int s = rowst[tid];
+      if (s >= 0) {
+        const float* in = H + ((nl - 2) & 1) * M2_ROWS * hld + tid * hld;
+        float prob[8];
+        float mx = -__builtin_inff();
+        for (int c = 0; c < nout; ++c) {
+          float acc1 = 0.f;
+          for (int k = 0; k < Klast; ++k) acc1 = fmaf(in[k], wl[k * nout + c], acc1);
+          prob[c] = acc1 + bl[c];
+          mx = prob[c] > mx ? prob[c] : mx;
+        }
+        float den = 0.f;
+        for (int c = 0; c < nout; ++c) {
+          prob[c] = expf(prob[c] - mx);
+          den += prob[c];
+        }
+        const double f1 = (double)(prob[a.s.min_class[s]] / den);
+        const int i = r0 + tid - s * a.n;
+        if (a.F) {
+          const int orow = a.out_map ? a.out_map[(size_t)s * a.n + i] : i;
+          a.F[((size_t)s * a.out_rows + orow) * 3] = f1;
+        }
+        if (a.hist) a.hist[((size_t)s * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
+      }
+    }
+  }
+}
+
 // Classifier.predict_proba: 32 rows per workgroup, full-width first layer.
 template <int MAXCT>
 __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
@@ -1227,8 +1433,36 @@ hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
   return launch_cons(a, slot, hist_row0, stream);
 }
 
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      n = prop.multiProcessorCount;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <int CJ>
+static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_mlp2<CJ>);
+    configured = true;
+  }
+  const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
+  const int grid = ntiles < 2 * cu_count() ? ntiles : 2 * cu_count();
+  hipLaunchKernelGGL((k_mlp2<CJ>), dim3(grid), dim3(256), mlp2_lds(a.p), stream, slot, hist_row0);
+  return hipGetLastError();
+}
+
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
+  if (a.p.mlp2 && !std::getenv("MV_MLP_V1"))
+    return mlp2_hmax(a.p) <= 64 ? mlp2_go<1>(a, slot, hist_row0, stream)
+                                : mlp2_go<2>(a, slot, hist_row0, stream);
   configure_lds_once();
   const int nl = a.p.n_layers;
   const int hmax = max_hidden(a.p.dims, nl);

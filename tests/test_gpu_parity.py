@@ -291,6 +291,19 @@ def test_attack_deterministic_and_batch_invariant():
     np.testing.assert_array_equal(F1.cpu().numpy()[2:], F3.cpu().numpy())
 
 
+def test_attack_state_groups_bit_identical(monkeypatch):
+    """mv_attack_run splits the states into groups on separate streams (MV_GROUPS): the
+    populations must not depend on the grouping."""
+    p = Project("botnet")
+    X = p.x[:9]
+    monkeypatch.setenv("MV_GROUPS", "1")
+    _, g1, F1, _, _ = _attack("botnet", X, 4, 5)
+    monkeypatch.setenv("MV_GROUPS", "4")
+    _, g4, F4, _, _ = _attack("botnet", X, 4, 5)
+    np.testing.assert_array_equal(g1.cpu().numpy(), g4.cpu().numpy())
+    np.testing.assert_array_equal(F1.cpu().numpy(), F4.cpu().numpy())
+
+
 def test_moeva2_generate_api_lcld():
     from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
     from moeva2_amd.attacks.moeva2.utils import results_to_history, results_to_numpy_results
