@@ -455,7 +455,8 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int g = lane + 64 * t;
-      ginf[t] = g < V ? gi[g] : 0;
+      const int w = gi[g < V ? g : V - 1];  // unconditional load (see k_cons load_row)
+      ginf[t] = g < V ? w : 0;
       if (REGC) {
         const bool in = ev && g < Dm4;
         cS[t] = in ? mS[g] : 0.0;
@@ -537,29 +538,34 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
           mu[q] = u;
         }
     }
-    // (2) crossed parent values at those positions (independent loads), (3) mutate
-#pragma unroll
-    for (int q = 0; q < MUT_CAP; ++q) {
-      if (q < cnt) {
-        const bool sw = swapped_packed(s_ginfo[mpos[q]], cx0_v, cx1_v);
-        mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mpos[q]];
-      }
-    }
+    // (2) crossed parent values and gene bounds at those positions: independent,
+    // unconditional loads (clamped position; unused slots are never applied), (3) mutate
     const double* gl = a.s.gl + (size_t)b * V;
     const double* gu = a.s.gu + (size_t)b * V;
+    double mlo[MUT_CAP], mhi[MUT_CAP];
+#pragma unroll
+    for (int q = 0; q < MUT_CAP; ++q) {
+      const int mp = mpos[q] < 0 ? 0 : mpos[q];
+      const bool sw = swapped_packed(s_ginfo[mp], cx0_v, cx1_v);
+      mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mp];
+      mlo[q] = gl[mp];
+      mhi[q] = gu[mp];
+    }
 #pragma unroll 1
     for (int q = 0; q < MUT_CAP && __ballot(q < cnt); ++q) {
       int gp = 0;
-      double xv = 0.0, u = 0.0;
+      double xv = 0.0, u = 0.0, lo = 0.0, hi = 0.0;
 #pragma unroll
       for (int r = 0; r < MUT_CAP; ++r)
         if (r == q) {
           gp = mpos[r];
           xv = mval[r];
           u = mu[r];
+          lo = mlo[r];
+          hi = mhi[r];
         }
       if (q < cnt) {
-        xv = mutate_gene(xv, gl[gp], gu[gp], (s_ginfo[gp] & 3) == 0, u, a.eta);
+        xv = mutate_gene(xv, lo, hi, (s_ginfo[gp] & 3) == 0, u, a.eta);
 #pragma unroll
         for (int r = 0; r < MUT_CAP; ++r)
           if (r == q) mval[r] = xv;
@@ -583,7 +589,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int g = lane + 64 * t;
-      if (g < Vo) x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g];
+      x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g < Vo ? g : Vo - 1];
     }
   };
   const bool l2 = p.norm == 2;
@@ -723,7 +729,11 @@ __global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_
   {
     const int* gi = (const int*)(p.vblob + o.ginfo);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) ginf[t] = lane + 64 * t < V ? gi[lane + 64 * t] : 0;
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      const int w = gi[g < V ? g : V - 1];
+      ginf[t] = g < V ? w : 0;
+    }
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -757,11 +767,15 @@ __global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_
   }
   const double* gsrc = a.mode == 1 ? a.genes_out + (size_t)b * a.out_rows * V
                                    : a.genes_in + (size_t)b * a.in_rows * V;
+  // Unconditional (index-clamped) loads: a per-element "if (g < V) load" makes hipcc branch
+  // around each load and wait vmcnt(0) per element, serialising the row's round trips.
   auto load_row = [&](int k, double* x) {
     const double* gr = gsrc + (size_t)rdl(src_v, k) * V;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      if (lane + 64 * t < V) x[t] = gr[lane + 64 * t];
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      x[t] = gr[g < V ? g : V - 1];
+    }
   };
   double xn[NT];
   if (nrw > 0) load_row(0, xn);
@@ -988,29 +1002,56 @@ __host__ __device__ inline size_t mlp2_head(const DProblem& p) {
   const int nl = p.n_layers;
   return 256 + (((size_t)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~(size_t)15);
 }
+// The hidden ping-pong H aliases the layer-0 chunk buffers (free once layer 0 is done), so
+// four workgroups fit a CU's LDS.
+__host__ __device__ inline int mlp2_region_floats(const DProblem& p) {
+  const int a0 = 2 * M2_ROWS * M2_ALD, h = 2 * M2_ROWS * (mlp2_hmax(p) + 4);
+  return a0 > h ? a0 : h;
+}
+// The final layer's per-wave partial sums [4][M2_ROWS][n_out] go to the free half of the
+// ping-pong when they fit there, else after the region.
+__host__ __device__ inline bool mlp2_part_inplace(const DProblem& p) {
+  return 4 * p.dims[p.n_layers] <= mlp2_hmax(p) + 4;
+}
 __host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
-  const size_t hld = mlp2_hmax(p) + 4;
-  return mlp2_head(p) + (size_t)2 * M2_ROWS * M2_ALD * 4 + 2 * M2_ROWS * hld * 4;
+  return mlp2_head(p) + (size_t)mlp2_region_floats(p) * 4 +
+         (mlp2_part_inplace(p) ? 0 : (size_t)4 * M2_ROWS * p.dims[p.n_layers] * 4);
+}
+
+// A wave's share of a layer's (column tile, row tile) grid: column tiles cb + 4cj over all
+// four row tiles when the layer has >= 3 column tiles, else the waves also split the row
+// tiles (N = 32: two waves per column tile, N = 16: one row tile per wave).
+struct TileMap {
+  int cb, rt0, nrt;
+};
+__device__ __forceinline__ TileMap tile_map(int nct, int wave) {
+  const int cw = nct >= 3 ? 4 : nct;
+  return TileMap{wave % cw, (wave / cw) * cw, cw};
 }
 
 template <int CJ>
 __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
                                            const float* __restrict__ Wp, int nkg, int N,
-                                           floatx4 (&acc)[CJ][4], int wave, int il, int ka) {
+                                           floatx4 (&acc)[CJ][4], TileMap m, int il, int ka) {
   const int nct = N >> 4;
+  const int wave = m.cb;
+  // loads are unconditional with clamped indices (a conditional load makes hipcc branch and
+  // wait vmcnt(0), which would drain the next group's prefetch every step)
   auto load_b = [&](int kg, float4 (&bf)[CJ]) {
+    const int kgc = kg < nkg ? kg : nkg - 1;
 #pragma unroll
     for (int cj = 0; cj < CJ; ++cj) {
-      const int ct = wave + 4 * cj;
-      bf[cj] = (ct < nct && kg < nkg)
-                   ? *(const float4*)(Wp + ((size_t)kg * N + ct * 16 + il) * 16 + 4 * ka)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int ct = wave + 4 * cj < nct ? wave + 4 * cj : nct - 1;
+      bf[cj] = *(const float4*)(Wp + ((size_t)kgc * N + ct * 16 + il) * 16 + 4 * ka);
     }
   };
   auto load_a = [&](int kg, float4 (&af)[4]) {
+    const int kgc = kg < nkg ? kg : nkg - 1;
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
-      af[rt] = *(const float4*)(A + (rt * 16 + il) * lda + kg * 16 + 4 * ka);
+    for (int rt = 0; rt < 4; ++rt) {
+      const int r = m.rt0 + (rt < m.nrt ? rt : 0);
+      af[rt] = *(const float4*)(A + (r * 16 + il) * lda + kgc * 16 + 4 * ka);
+    }
   };
   float4 bf[CJ], af[4];
   load_b(0, bf);
@@ -1018,12 +1059,13 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
   for (int kg = 0; kg < nkg; ++kg) {
     float4 bn[CJ], an[4];
     load_b(kg + 1, bn);  // next group's weights (L2) while this group's MFMAs run
-    if (kg + 1 < nkg) load_a(kg + 1, an);
+    load_a(kg + 1, an);
 #pragma unroll
     for (int cj = 0; cj < CJ; ++cj) {
       if (wave + 4 * cj < nct) {
 #pragma unroll
         for (int rt = 0; rt < 4; ++rt) {
+          if (rt >= m.nrt) continue;
           acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].x, bf[cj].x, acc[cj][rt], 0, 0, 0);
           acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].y, bf[cj].y, acc[cj][rt], 0, 0, 0);
           acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].z, bf[cj].z, acc[cj][rt], 0, 0, 0);
@@ -1033,15 +1075,13 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
     }
 #pragma unroll
     for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
-    if (kg + 1 < nkg) {
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt) af[rt] = an[rt];
-    }
+    for (int rt = 0; rt < 4; ++rt) af[rt] = an[rt];
   }
 }
 
 template <int CJ>
-__global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
+__global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
@@ -1055,7 +1095,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
   float* wl = (float*)(smem + 256);
   float* bl = wl + Klast * nout;
   float* A0 = (float*)(smem + mlp2_head(p));
-  float* H = A0 + 2 * M2_ROWS * M2_ALD;
+  float* H = A0;  // hidden ping-pong, aliases the layer-0 chunks
   for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
   if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
@@ -1069,10 +1109,11 @@ __global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
       for (int u = 0; u < 4; ++u) {
         const int idx = tid + 256 * u;
         const int row = idx >> 4, q = idx & 15;
-        const int k = c * 64 + 4 * q;
-        st[u] = (r0 + row < a.total && k < K0)
-                    ? *(const float4*)(a.xml + (size_t)(r0 + row) * K0 + k)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        // clamped, unconditional loads: rows past the end are computed but never written,
+        // k past K0 is never multiplied (the last chunk runs only its nkg0 % 4 groups)
+        const int k = c * 64 + 4 * q < K0 ? c * 64 + 4 * q : K0 - 4;
+        const int rr = r0 + row < a.total ? r0 + row : a.total - 1;
+        st[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);
       }
     };
     auto chunk_store = [&](int buf) {
@@ -1097,32 +1138,34 @@ __global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
       if (c + 1 < nch) chunk_load(c + 1);
       const int ng = min(4, nkg0 - 4 * c);
       mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, p.Wp[0] + (size_t)4 * c * N0 * 16,
-                     ng, N0, acc, wave, il, ka);
+                     ng, N0, acc, tile_map(N0 >> 4, wave), il, ka);
       if (c + 1 < nch) chunk_store((c + 1) & 1);
       __syncthreads();
     }
     // hidden layers: layer l writes H[l & 1]
     for (int l = 0; l + 1 < nl; ++l) {
       const int N = p.dims[l + 1];
+      const TileMap m = tile_map(N >> 4, wave);
       if (l > 0) {
 #pragma unroll
         for (int cj = 0; cj < CJ; ++cj)
 #pragma unroll
           for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
         mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N, acc,
-                       wave, il, ka);
+                       m, il, ka);
       }
       float* out = H + (l & 1) * M2_ROWS * hld;
 #pragma unroll
       for (int cj = 0; cj < CJ; ++cj) {
-        const int ct = wave + 4 * cj;
+        const int ct = m.cb + 4 * cj;
         if (ct < (N >> 4)) {
           const int col = ct * 16 + il;
 #pragma unroll
           for (int rt = 0; rt < 4; ++rt) {
+            if (rt >= m.nrt) continue;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const int row = rt * 16 + ka * 4 + j;
+              const int row = (m.rt0 + rt) * 16 + ka * 4 + j;
               float bv;
               if (l == 0) {
                 const int s = rowst[row];
@@ -1138,17 +1181,43 @@ __global__ __launch_bounds__(256, 2) void k_mlp2(int slot, int hist_row0) {
       }
       __syncthreads();
     }
-    // final Dense + softmax (classifier.py:23-29) -> f1
+    // final Dense + softmax (classifier.py:23-29) -> f1.  Wave w sums the k quarter
+    // [w Klast/4, (w+1) Klast/4) of every row (lane = row), wave 0 combines and normalises.
+    float* part = mlp2_part_inplace(p) ? H + ((nl - 1) & 1) * M2_ROWS * hld
+                                       : A0 + mlp2_region_floats(p);
+    {
+      const int kq = Klast >> 2;
+      const float* ir = H + ((nl - 2) & 1) * M2_ROWS * hld + lane * hld + wave * kq;
+      const float* wq = wl + wave * kq * nout;
+      float ps[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) ps[c] = 0.f;
+      for (int k = 0; k < kq; k += 4) {
+        const float4 v = *(const float4*)(ir + k);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (c < nout) {
+            ps[c] = fmaf(v.x, wq[k * nout + c], ps[c]);
+            ps[c] = fmaf(v.y, wq[(k + 1) * nout + c], ps[c]);
+            ps[c] = fmaf(v.z, wq[(k + 2) * nout + c], ps[c]);
+            ps[c] = fmaf(v.w, wq[(k + 3) * nout + c], ps[c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c < nout) part[(wave * M2_ROWS + lane) * nout + c] = ps[c];
+    }
+    __syncthreads();
     if (tid < M2_ROWS) {
       const int s = rowst[tid];
       if (s >= 0) {
-        const float* in = H + ((nl - 2) & 1) * M2_ROWS * hld + tid * hld;
         float prob[8];
         float mx = -__builtin_inff();
         for (int c = 0; c < nout; ++c) {
-          float acc1 = 0.f;
-          for (int k = 0; k < Klast; ++k) acc1 = fmaf(in[k], wl[k * nout + c], acc1);
-          prob[c] = acc1 + bl[c];
+          const float* q = part + tid * nout + c;
+          prob[c] = (((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
+                     q[3 * M2_ROWS * nout]) + bl[c];
           mx = prob[c] > mx ? prob[c] : mx;
         }
         float den = 0.f;
@@ -1448,13 +1517,25 @@ static int cu_count() {
 template <int CJ>
 static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static bool configured = false;
+  static size_t occ_lds = 0;
+  static int occ = 2;
   if (!configured) {
     allow_lds(k_mlp2<CJ>);
     configured = true;
   }
+  const size_t lds = mlp2_lds(a.p);
+  if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ>, 256, lds) != hipSuccess ||
+        n < 1)
+      n = 1;
+    (void)hipGetLastError();
+    occ = n;
+    occ_lds = lds;
+  }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
-  const int grid = ntiles < 2 * cu_count() ? ntiles : 2 * cu_count();
-  hipLaunchKernelGGL((k_mlp2<CJ>), dim3(grid), dim3(256), mlp2_lds(a.p), stream, slot, hist_row0);
+  const int grid = ntiles < occ * cu_count() ? ntiles : occ * cu_count();
+  hipLaunchKernelGGL((k_mlp2<CJ>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 

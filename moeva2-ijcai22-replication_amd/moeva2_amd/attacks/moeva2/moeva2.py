@@ -124,6 +124,18 @@ class Moeva2:
         hist_h = hist.cpu().numpy() if hist is not None else None
         return [self._result(b, x[b], genes_h[b], F_h[b], hist_h, P, O) for b in range(B)]
 
+    def generate_sharded(self, x: np.ndarray, minimize_class, group=None):
+        """Multi-GPU form of generate: this rank attacks its contiguous slice of the states
+        (moeva2_amd.distributed.shard_bounds) on its own GPU and one all_gather returns the
+        final populations of every state to every rank: genes (B, P, V), F (B, P, 3)."""
+        from ...distributed import generate_sharded
+
+        def attack(xs, mcs):
+            genes, F, _ = self.generate(xs, mcs, return_device=True)
+            return genes, F
+
+        return generate_sharded(attack, x, minimize_class, group)
+
     def _result(self, b, x0, genes, F, hist, P, O):
         pop = Population(Individual(genes[i], F[i]) for i in range(P))
         nd = _non_dominated(F)

@@ -1,0 +1,63 @@
+"""The N>1 path on CPU: world_size-2 gloo process group, sharding of the initial states and
+the final all_gather (moeva2_amd.distributed), against the unsharded computation."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def fake_attack(x, mc):
+    """A deterministic per-state stand-in for Moeva2.generate(return_device=True)."""
+    xs = torch.as_tensor(np.asarray(x, np.float64))
+    genes = xs[:, None, :].repeat(1, 3, 1) * torch.arange(1, 4, dtype=torch.float64)[None, :, None]
+    F = torch.stack([xs.sum(1), xs.max(1).values, torch.as_tensor(mc, dtype=torch.float64)], 1)
+    return genes, F[:, None, :]
+
+
+def _worker(rank, world, port, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from moeva2_amd.distributed import generate_sharded
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
+    genes, F = generate_sharded(fake_attack, x, np.arange(B) % 2)
+    q.put((rank, genes.numpy(), F.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [7, 8, 1])
+def test_sharded_attack_gathers_every_state(B):
+    import torch.multiprocessing as mp
+
+    from moeva2_amd.distributed import shard_bounds
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, B, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
+    ref_g, ref_F = fake_attack(x, np.arange(B) % 2)
+    for _, genes, F in res:  # every rank holds every state, in state order
+        np.testing.assert_array_equal(genes, ref_g.numpy())
+        np.testing.assert_array_equal(F, ref_F.numpy())
+    assert [shard_bounds(B, 2, r) for r in range(2)] == [(0, (B + 1) // 2), ((B + 1) // 2, B)]
