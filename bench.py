@@ -79,16 +79,19 @@ def cpu_baseline(w, sample_states=1, sample_gens=100):
 
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
+    from threadpoolctl import threadpool_limits
+
     p = Project(w["project"])
     ref = energy_ref_dirs(3, w["n_pop"], seed=1)
     P, O = w["n_pop"] + 3, w["n_off"]
-    t0 = time.perf_counter()
     n_eval = 0
-    for s in range(sample_states):
-        mo.run_attack(p.problem(p.x[s], norm=w["norm"]), ref, sample_gens, P, O, seed=42,
-                      save_history=w["history"])
-        n_eval += P + (sample_gens - 1) * O
-    dt = time.perf_counter() - t0
+    with threadpool_limits(limits=1):  # one core: BLAS in the numpy MLP stays single-threaded
+        t0 = time.perf_counter()
+        for s in range(sample_states):
+            mo.run_attack(p.problem(p.x[s], norm=w["norm"]), ref, sample_gens, P, O, seed=42,
+                          save_history=w["history"])
+            n_eval += P + (sample_gens - 1) * O
+        dt = time.perf_counter() - t0
     return {"value": n_eval / dt, "unit": "evals/s", "cores": 1, "kind": "port",
             "sample": f"{sample_states} {w['project']} state(s) x {sample_gens} generations "
                       f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack, numpy, 1 process",
@@ -103,9 +106,16 @@ def main():
     ap.add_argument("--workload", default="rq1.botnet.static", choices=sorted(WORKLOADS))
     ap.add_argument("--n-gen", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-gens", type=int, default=100)
+    ap.add_argument("--groups", type=int, default=None,
+                    help="state groups (streams) of the timed attack; default: engine's choice. "
+                         "--groups 1 makes every launch cover all states, like the roofline "
+                         "pass, so rocprofv3 averages compare 1:1 with the bench's event times")
+    ap.add_argument("--cpu-gens", type=int, default=300)
+    ap.add_argument("--cpu-states", type=int, default=2)
     args = ap.parse_args()
 
+    if args.groups:
+        os.environ["MV_GROUPS"] = str(args.groups)
     import torch
     import torch.distributed as dist
 
@@ -201,22 +211,32 @@ def main():
     dims = [Dm] + list(eng_dims(eng))[1:]
     mlp_flops = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
 
-    def hbm(name, bytes_launch, ms):
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of this workload
+    # (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH correction)
+    traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if w["project"] == "botnet" and os.path.exists(tpath):
+        with open(tpath) as fh:
+            traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()}
+
+    def hbm(name, bytes_launch, ms, key):
         gbs = bytes_launch / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs / HBM_PEAK_GBS, "traffic": None, "kernel": name,
+                "frac": gbs / HBM_PEAK_GBS, "traffic": traffic.get(key), "kernel": name,
                 "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": ms}
 
     kernels = {
-        "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows, gen_ms),
-        "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms),
+        "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows, gen_ms,
+                     "k_gen"),
+        "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
+                      "k_cons"),
         "k_mlp": {"bound": "mfma", "achieved": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12,
                   "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                   "frac": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
-                  "traffic": None, "kernel": "k_mlp (fp32 MFMA Dense chain)",
+                  "traffic": traffic.get("k_mlp"), "kernel": "k_mlp (fp32 MFMA Dense chain)",
                   "algorithmic_flops_per_launch": mlp_flops * rows, "avg_launch_ms": mlp_ms},
         "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
-                         surv_bytes_state * B, surv_ms),
+                         surv_bytes_state * B, surv_ms, "k_survive"),
     }
     dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
 
@@ -247,7 +267,7 @@ def main():
                                           "k_survive": surv_ms, "dominant": dom},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        result["cpu_baseline"] = cpu_baseline(w, 1, args.cpu_gens)
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_states, args.cpu_gens)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
