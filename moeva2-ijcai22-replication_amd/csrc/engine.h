@@ -19,6 +19,7 @@ constexpr int MAX_LAYERS = 6;
 constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
 constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
 constexpr int VARY_T = 256;      // threads per k_gen / k_cons workgroup (4 waves)
+constexpr int VARY_ROWS_MAX = 32; // rows of one state per k_gen / k_cons workgroup (swept: 16/32/64)
 constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
 constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS

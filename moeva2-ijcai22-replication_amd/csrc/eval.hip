@@ -1407,9 +1407,15 @@ static void allow_lds(K kern) {
   (void)hipGetLastError();
 }
 
-// Rows per k_gen / k_cons workgroup: chunks of at most 64 rows of one state, balanced.
+// Rows per k_gen / k_cons workgroup: chunks of at most VARY_ROWS_MAX rows of one state,
+// balanced (MV_VARY_ROWS overrides the cap; development sweeps).
 static int vary_rows_per_wg(int n) {
-  const int nchunk = (n + 63) / 64;
+  static int cap = [] {
+    const char* s = std::getenv("MV_VARY_ROWS");
+    const int v = s ? std::atoi(s) : VARY_ROWS_MAX;
+    return v < 4 ? 4 : (v > 64 ? 64 : v);
+  }();
+  const int nchunk = (n + cap - 1) / cap;
   return (n + nchunk - 1) / nchunk;
 }
 
