@@ -140,6 +140,33 @@ int mv_mlp_create(int32_t device, const mv_model_desc* model, mv_mlp** out);
 void mv_mlp_destroy(mv_mlp* m);
 int mv_mlp_predict(mv_mlp* m, int32_t n, const double* x, double* proba, void* stream);
 
+/* ObjectiveCalculator._calculate_objective (objective_calculator.py:44-84) batched over B
+ * initial states x n candidates (ML space), the scoring behind success_rate_3d (:106-119)
+ * and get_successful_attacks (:152-223).  Per row: CV = calc_constraint_violation of
+ * [constraints.evaluate(x) | get_one_hot_encoding_constraints(type_mask, x)] (utils.py:43-54),
+ * f1 = predict_proba(ml_scaler(x))[:, minimize_class], f2 = ||mm(x_init) - mm(x)||_{2|inf}
+ * on the min_max_scaler.  The constraint program is taken from a (model-less) engine, the
+ * classifier from an mv_mlp. */
+typedef struct mv_objcalc_desc {
+  int32_t D;                  /* ML feature count */
+  int32_t n_ohe;              /* one-hot groups of the FULL type mask, get_ohe_masks order */
+  const int32_t* ohe_offsets; /* host [n_ohe+1] CSR offsets */
+  const int32_t* ohe_feats;   /* host [..] features of each group */
+  const double* mm_scale;     /* host [D] min_max_scaler scale_ (distance) */
+  const double* mm_min;       /* host [D] min_max_scaler min_ */
+  const double* ml_scale;     /* host [D] ml_scaler scale_, or NULL (ml_scaler None) */
+  const double* ml_min;       /* host [D] or NULL */
+  int32_t norm;               /* 2 = L2, 0 = Linf */
+} mv_objcalc_desc;
+typedef struct mv_objcalc mv_objcalc;
+int mv_objcalc_create(int32_t device, const mv_objcalc_desc* desc, mv_objcalc** out);
+void mv_objcalc_destroy(mv_objcalc* o);
+/* x_init dev [B][D], x dev [B][n][D] -> obj dev [B][n][3] (CV, f1, f2) and range_bad dev
+ * [B][n] (1 where the scaled row or origin leaves [-1e-4, 1+1e-4]: the reference asserts,
+ * objective_calculator.py:72-76). */
+int mv_objcalc_run(mv_objcalc* o, mv_engine* constraints, mv_mlp* classifier, int32_t B,
+                   int32_t n, const double* x_init, const double* x, int32_t minimize_class,
+                   double* obj, int32_t* range_bad, void* stream);
 typedef struct mv_attack_params {
   int32_t n_gen;          /* Moeva2 n_gen (termination "n_gen") */
   int32_t pop_size;       /* P = n_ref_points + n_obj (203 for n_pop 200) */

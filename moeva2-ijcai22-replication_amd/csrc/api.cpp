@@ -900,6 +900,138 @@ int mv_mlp_predict(mv_mlp* m, int32_t n, const double* x, double* proba, void* s
   return MV_OK;
 }
 
+struct mv_objcalc {
+  int device = 0;
+  int D = 0, n_ohe = 0, norm = 2;
+  int* ohe_off = nullptr;
+  int* ohe_feat = nullptr;
+  double *mm_s = nullptr, *mm_m = nullptr, *ml_s = nullptr, *ml_m = nullptr;
+  double *xml = nullptr, *G = nullptr, *proba = nullptr;
+  size_t cap_xml = 0, cap_G = 0, cap_p = 0;
+  std::vector<void*> allocs;
+  ~mv_objcalc() {
+    (void)hipSetDevice(device);
+    for (void* x : allocs) (void)hipFree(x);
+    (void)hipFree(xml);
+    (void)hipFree(G);
+    (void)hipFree(proba);
+  }
+};
+
+int mv_objcalc_create(int32_t device, const mv_objcalc_desc* d, mv_objcalc** out) {
+  if (!d || !out || d->D <= 0 || d->n_ohe < 0 || !d->mm_scale || !d->mm_min ||
+      (d->n_ohe > 0 && (!d->ohe_offsets || !d->ohe_feats)) ||
+      ((d->ml_scale == nullptr) != (d->ml_min == nullptr)) || (d->norm != 2 && d->norm != 0))
+    return fail(MV_ERR_ARG, "bad mv_objcalc_desc");
+  *out = nullptr;
+  for (int g = 0; g < d->n_ohe; ++g)
+    if (d->ohe_offsets[g + 1] < d->ohe_offsets[g]) return fail(MV_ERR_ARG, "ohe offsets");
+  const int nf = d->n_ohe > 0 ? d->ohe_offsets[d->n_ohe] : 0;
+  for (int k = 0; k < nf; ++k)
+    if (d->ohe_feats[k] < 0 || d->ohe_feats[k] >= d->D) return fail(MV_ERR_ARG, "ohe feature");
+  HIPCHK(hipSetDevice(device));
+  mv_objcalc* o = new mv_objcalc();
+  o->device = device;
+  o->D = d->D;
+  o->n_ohe = d->n_ohe;
+  o->norm = d->norm;
+  std::vector<int> off(d->n_ohe + 1, 0), feat(nf > 0 ? nf : 1, 0);
+  for (int g = 0; g <= d->n_ohe && d->n_ohe > 0; ++g) off[g] = d->ohe_offsets[g];
+  for (int k = 0; k < nf; ++k) feat[k] = d->ohe_feats[k];
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err != hipSuccess) return;
+    err = upload(dst, host, n);
+    if (err == hipSuccess) o->allocs.push_back((void*)*dst);
+  };
+  K(&o->ohe_off, off.data(), off.size());
+  K(&o->ohe_feat, feat.data(), feat.size());
+  K(&o->mm_s, d->mm_scale, (size_t)d->D);
+  K(&o->mm_m, d->mm_min, (size_t)d->D);
+  if (d->ml_scale) {
+    K(&o->ml_s, d->ml_scale, (size_t)d->D);
+    K(&o->ml_m, d->ml_min, (size_t)d->D);
+  }
+  if (err != hipSuccess) {
+    delete o;
+    return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
+  }
+  *out = o;
+  return MV_OK;
+}
+
+void mv_objcalc_destroy(mv_objcalc* o) { delete o; }
+
+static hipError_t grow(double** p, size_t* cap, size_t n) {
+  if (n <= *cap) return hipSuccess;
+  hipError_t e = hipDeviceSynchronize();  // earlier launches may still read the old buffer
+  if (e != hipSuccess) return e;
+  (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  e = hipMalloc((void**)p, n * sizeof(double));
+  if (e == hipSuccess) *cap = n;
+  return e;
+}
+
+int mv_objcalc_run(mv_objcalc* o, mv_engine* e, mv_mlp* m, int32_t B, int32_t n,
+                   const double* x_init, const double* x, int32_t minimize_class, double* obj,
+                   int32_t* range_bad, void* stream_) {
+  if (!o || !e || !m || B < 0 || n < 0) return fail(MV_ERR_ARG, "bad mv_objcalc_run arguments");
+  if (e->p.D != o->D || m->a.dims[0] != o->D)
+    return fail(MV_ERR_ARG, "constraints / classifier / scaler feature counts differ");
+  const int n_out = m->a.dims[m->a.n_layers];
+  if (minimize_class < 0 || minimize_class >= (n_out == 1 ? 2 : n_out))
+    return fail(MV_ERR_ARG, "minimize_class outside the classifier output");
+  const long total = (long)B * n;
+  if (total == 0) return MV_OK;
+  if (!x_init || !x || !obj || !range_bad) return fail(MV_ERR_ARG, "null buffer");
+  if (e->device != o->device || m->device != o->device)
+    return fail(MV_ERR_ARG, "objects live on different devices");
+  hipStream_t stream = (hipStream_t)stream_;
+  HIPCHK(hipSetDevice(o->device));
+  HIPCHK(grow(&o->G, &o->cap_G, (size_t)total * (e->p.C > 0 ? e->p.C : 1)));
+  HIPCHK(grow(&o->proba, &o->cap_p, (size_t)total * n_out));
+  const double* xml = x;
+  if (o->ml_s) {
+    HIPCHK(grow(&o->xml, &o->cap_xml, (size_t)total * o->D));
+    HIPCHK(launch_obj_mlscale(total * o->D, o->D, x, o->ml_s, o->ml_m, o->xml, stream));
+    xml = o->xml;
+  }
+  if (e->p.C > 0) {
+    int slot = 0;
+    HIPCHK(stage_rows(base_rows(e), stream, &slot));
+    HIPCHK(launch_constraints(e->p, slot, (int)total, x, o->G, stream));
+    HIPCHK(release_rows(slot, stream));
+  }
+  MlpArgs ma = m->a;
+  ma.n = (int)total;
+  ma.x = xml;
+  ma.proba = o->proba;
+  HIPCHK(launch_predict(ma, stream));
+  ObjArgs a{};
+  a.total = total;
+  a.n = n;
+  a.D = o->D;
+  a.C = e->p.C;
+  a.n_ohe = o->n_ohe;
+  a.n_out = n_out;
+  a.cls = minimize_class;
+  a.norm = o->norm;
+  a.x = x;
+  a.x_init = x_init;
+  a.mm_scale = o->mm_s;
+  a.mm_min = o->mm_m;
+  a.ohe_off = o->ohe_off;
+  a.ohe_feat = o->ohe_feat;
+  a.G = o->G;
+  a.proba = o->proba;
+  a.obj = obj;
+  a.range_bad = range_bad;
+  HIPCHK(launch_objectives(a, stream));
+  return MV_OK;
+}
+
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
   if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
   HIPCHK(hipSetDevice(e->device));

@@ -153,4 +153,21 @@ struct MlpArgs {
   double* proba;                  // [n][n_out]
 };
 
+// ObjectiveCalculator._calculate_objective (objectives.hip) -------------------------------
+struct ObjArgs {
+  long total;                     // B * n rows
+  int n;                          // rows per state
+  int D, C, n_ohe, n_out, cls, norm;
+  const double* x;                // [B][n][D] ML-space candidates
+  const double* x_init;           // [B][D]
+  const double* mm_scale;         // [D] min_max_scaler (distance)
+  const double* mm_min;           // [D]
+  const int* ohe_off;             // [n_ohe+1] full-type-mask one-hot groups
+  const int* ohe_feat;
+  const double* G;                // [B*n][C] constraints (tol-clamped)
+  const double* proba;            // [B*n][n_out]
+  double* obj;                    // [B][n][3]: CV, f1, f2
+  int* range_bad;                 // [B][n]: scaled row or origin outside [-1e-4, 1+1e-4]
+};
+
 }  // namespace mv

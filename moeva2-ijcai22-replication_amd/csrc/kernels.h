@@ -138,6 +138,9 @@ hipError_t launch_select(int B, int P, int O, uint64_t seed, uint32_t stream_key
                          const int* pop_slot, int* parents, hipStream_t stream);
 hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* genes0,
                             double* pool, int* pop_slot, int* free_slot, hipStream_t stream);
+hipError_t launch_obj_mlscale(long total, int D, const double* x, const double* s,
+                              const double* m, double* out, hipStream_t stream);
+hipError_t launch_objectives(const ObjArgs& a, hipStream_t stream);
 hipError_t launch_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
                              const double* poolF, double* genes, double* F, hipStream_t stream);
 

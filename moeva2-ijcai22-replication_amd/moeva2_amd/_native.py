@@ -25,7 +25,7 @@ EXPORTED = [
     "mv_set_states", "mv_evaluate", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
     "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_mlp_create", "mv_mlp_destroy",
-    "mv_mlp_predict",
+    "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -53,6 +53,12 @@ class AttackParams(C.Structure):
     _fields_ = [("n_gen", C.c_int32), ("pop_size", C.c_int32), ("n_offsprings", C.c_int32),
                 ("seed", C.c_uint64), ("n_ref", C.c_int32), ("ref_points", _f64p),
                 ("mu", C.c_double), ("history", C.c_int32)]
+
+
+class ObjCalcDesc(C.Structure):
+    _fields_ = [("D", C.c_int32), ("n_ohe", C.c_int32), ("ohe_offsets", _i32p),
+                ("ohe_feats", _i32p), ("mm_scale", _f64p), ("mm_min", _f64p),
+                ("ml_scale", _f64p), ("ml_min", _f64p), ("norm", C.c_int32)]
 
 
 class NativeError(RuntimeError):
@@ -92,6 +98,8 @@ def lib():
             "mv_get_phase_times": [vp, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
+            "mv_objcalc_create": [C.c_int32, C.POINTER(ObjCalcDesc), C.POINTER(vp)],
+            "mv_objcalc_run": [vp, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp, vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -101,6 +109,8 @@ def lib():
         L.mv_engine_destroy.restype = None
         L.mv_mlp_destroy.argtypes = [vp]
         L.mv_mlp_destroy.restype = None
+        L.mv_objcalc_destroy.argtypes = [vp]
+        L.mv_objcalc_destroy.restype = None
         _LIB = L
     return _LIB
 
@@ -328,6 +338,54 @@ class Mlp:
 
     def predict(self, x, proba, stream=None):
         check(lib().mv_mlp_predict(self._h, x.shape[0], _ptr(x), _ptr(proba), _stream(stream)))
+
+
+class ObjCalc:
+    """Device ObjectiveCalculator._calculate_objective (mv_objcalc_*): one per (type mask,
+    min_max_scaler, ml_scaler, norm)."""
+
+    def __init__(self, D, ohe_groups, mm_scale, mm_min, ml_scale=None, ml_min=None, norm=2,
+                 device=0):
+        keep = []
+
+        def P(a, dt, ct):
+            a = np.ascontiguousarray(a, dt)
+            keep.append(a)
+            return a.ctypes.data_as(C.POINTER(ct))
+
+        offs = np.zeros(len(ohe_groups) + 1, np.int32)
+        for g, m in enumerate(ohe_groups):
+            offs[g + 1] = offs[g] + len(m)
+        feats = (np.concatenate([np.asarray(m, np.int32) for m in ohe_groups])
+                 if ohe_groups else np.zeros(1, np.int32))
+        d = ObjCalcDesc()
+        d.D = int(D)
+        d.n_ohe = len(ohe_groups)
+        d.ohe_offsets = P(offs, np.int32, C.c_int32)
+        d.ohe_feats = P(feats, np.int32, C.c_int32)
+        d.mm_scale = P(mm_scale, np.float64, C.c_double)
+        d.mm_min = P(mm_min, np.float64, C.c_double)
+        if ml_scale is not None:
+            d.ml_scale = P(ml_scale, np.float64, C.c_double)
+            d.ml_min = P(ml_min, np.float64, C.c_double)
+        d.norm = 2 if norm in (2, "2") else 0
+        self._h = C.c_void_p()
+        check(lib().mv_objcalc_create(device, C.byref(d), C.byref(self._h)))
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _LIB is not None:
+            _LIB.mv_objcalc_destroy(h)
+            self._h = None
+
+    def run(self, engine: "Engine", mlp: "Mlp", x_init, x, minimize_class, obj, range_bad,
+            stream=None):
+        """x_init (B, D), x (B, n, D) device tensors -> obj (B, n, 3), range_bad (B, n)."""
+        B, n = int(x.shape[0]), int(x.shape[1])
+        check(lib().mv_objcalc_run(self._h, engine._h, mlp._h, B, n, _ptr(x_init), _ptr(x),
+                                   int(minimize_class), _ptr(obj), _ptr(range_bad),
+                                   _stream(stream)))
 
 
 _MLPS = {}

@@ -401,3 +401,80 @@ def test_success_rate_matches_oracle_attack():
     sr_cpu = mo.success_rate_3d(X, x_cpu, fn, 0.25, 0.2)
     print("identical final populations:", same, "/", B, "o1..o7 dev", sr_dev, "cpu", sr_cpu)
     assert np.all(np.abs(sr_dev - sr_cpu) <= max(0.01, 1.0 / B) + 1e-12), (sr_dev, sr_cpu)
+
+
+def _objcalc(name, norm=2, thr=(0.5, 4), ml=True):
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+
+    sc = make_scaler(name)
+    return ObjectiveCalculator(make_classifier(name), make_constraints(name), minimize_class=1,
+                               thresholds={"f1": thr[0], "f2": thr[1]}, min_max_scaler=sc,
+                               norm=norm, ml_scaler=sc if ml else None)
+
+
+def _check_obj(obj, ref):
+    """CV and f2 are fp64 sums (order differs from numpy): 1e-12 relative; f1 is fp32."""
+    np.testing.assert_allclose(obj[..., 0], ref[..., 0], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(obj[..., 1], ref[..., 1], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(obj[..., 2], ref[..., 2], rtol=1e-12, atol=1e-15)
+
+
+def test_objective_calculator_matches_reference_golden(golden):
+    """Device ObjectiveCalculator (mv_objcalc_run) against the reference's own
+    ObjectiveCalculator outputs (objective_calculator.py:44-119, golden vectors)."""
+    d = golden("objective_calculator_botnet.npz")
+    calc = _objcalc("botnet")
+    obj = calc.calculate_objectives_3d(d["x_init"], d["x_attacks"])
+    for i in range(4):
+        _check_obj(obj[i], d[f"obj{i}"])
+        np.testing.assert_array_equal(calc._objective_respected(obj[i]), d[f"resp{i}"])
+        np.testing.assert_array_equal(calc._objective_array(d["x_init"][i], d["x_attacks"][i]),
+                                      d[f"resp{i}"])
+    np.testing.assert_array_equal(calc.success_rate_3d(d["x_init"], d["x_attacks"]),
+                                  d["success_rate"])
+    assert list(calc.success_rate_3d_df(d["x_init"], d["x_attacks"]).columns) == \
+        [f"o{i}" for i in range(1, 8)]
+    sa, idx = calc.get_successful_attacks(d["x_init"], d["x_attacks"],
+                                          return_index_success=True)
+    assert idx.shape == (4,) and sa.shape[1] == 756
+
+
+@pytest.mark.parametrize("norm", [2, np.inf])
+def test_objective_calculator_lcld_ohe_against_oracle(norm):
+    """LCLD carries one-hot groups (utils.py:43-54): device objectives of attacked
+    populations against the oracle restatement, L2 and Linf, plus the success rates."""
+    p = Project("lcld")
+    X = p.x[:12]
+    _, g, _, _, _ = _attack("lcld", X, 6, 11, P=23, O=10)
+    genes = g.cpu().numpy()
+    xs = np.stack([mo.genetic_to_ml(p.lay, genes[b], X[b]) for b in range(X.shape[0])])
+    xs[:, 0] = X  # one exact origin per state
+    sc, mn = p.ml
+    calc = _objcalc("lcld", norm=norm, thr=(0.25, 0.2))
+    obj = calc.calculate_objectives_3d(X, xs)
+
+    def fn(xi, x):
+        return mo.objectives_calc(xi, x, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, "inf" if norm == np.inf else 2)
+
+    for b in range(X.shape[0]):
+        _check_obj(obj[b], fn(X[b], xs[b]))
+    np.testing.assert_array_equal(calc.success_rate_3d(X, xs),
+                                  mo.success_rate_3d(X, xs, fn, 0.25, 0.2))
+    # ragged list input takes the per-state path and agrees
+    np.testing.assert_array_equal(calc.success_rate_3d(X, [e for e in xs]),
+                                  calc.success_rate_3d(X, xs))
+
+
+def test_objective_calculator_range_assert():
+    """objective_calculator.py:72-76: a candidate outside the scaler range raises."""
+    p = Project("lcld")
+    X = p.x[:2]
+    xs = np.repeat(X[:, None], 3, axis=1).copy()
+    calc = _objcalc("lcld", thr=(0.25, 0.2))
+    calc.calculate_objectives_3d(X, xs)
+    sc, mn = p.ml
+    j = int(np.argmax(sc))
+    xs[1, 2, j] = (2.0 - mn[j]) / sc[j]  # scales to 2.0
+    with pytest.raises(AssertionError):
+        calc.calculate_objectives_3d(X, xs)
