@@ -478,3 +478,60 @@ def test_objective_calculator_range_assert():
     xs[1, 2, j] = (2.0 - mn[j]) / sc[j]  # scales to 2.0
     with pytest.raises(AssertionError):
         calc.calculate_objectives_3d(X, xs)
+
+
+def test_moeva_driver_outputs(tmp_path):
+    """04_moeva.py:27-142 output contract: results / x_attacks / x_history / metrics /
+    config files named by the config hash; metrics = ObjectiveCalculator success rates of
+    x_attacks; a second run with the same config is skipped."""
+    import json
+
+    from moeva2_amd.config_parser.config_parser import get_config, get_dict_hash
+    from moeva2_amd.experiments.united.moeva_run import run
+
+    cfg_dir = os.path.join(os.path.dirname(RES), "config")
+    c = get_config(["-c", f"{cfg_dir}/moeva.yaml", "-c", f"{cfg_dir}/rq1.lcld.static.yaml",
+                    "-p", "seed=42", "-p", "budget=5", "-p", "n_initial_state=6",
+                    "-p", f"dirs.results={tmp_path}", "-j", '{"eps_list":[0.2,0.4]}'])
+    h = get_dict_hash(c)
+    m = run(c, verbose=False)
+    xa = np.load(tmp_path / f"x_attacks_moeva_{h}.npy")
+    xh = np.load(tmp_path / f"x_history_moeva_{h}.npy")
+    assert xa.shape == (6, 203, 47) and xh.shape == (6, 4, 100, 13)
+    assert (tmp_path / f"results_{h}.npy").exists() and (tmp_path / f"config_moeva_{h}.yaml").exists()
+    on_disk = json.load(open(tmp_path / f"metrics_moeva_{h}.json"))
+    assert on_disk["config_hash"] == h and len(on_disk["objectives_list"]) == 2
+    assert list(on_disk["objectives_list"][0]) == [f"o{i}" for i in range(1, 8)]
+    p = Project("lcld")
+    sc, mn = p.ml
+
+    def fn(xi, x):
+        return mo.objectives_calc(xi, x, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, 2)
+
+    for k, eps in enumerate((0.2, 0.4)):
+        sr = mo.success_rate_3d(p.x[:6], xa, fn, 0.25, eps)
+        np.testing.assert_array_equal([m["objectives_list"][k][f"o{i}"] for i in range(1, 8)], sr)
+    assert run(c, verbose=False) is None
+
+
+def test_moeva_driver_augmented_reconstruction(tmp_path):
+    """rq4 form: lcld_augmented attack with the evaluation constraints and the
+    reconstruction branch (04_moeva.py:43-53, 97-103, 116-120)."""
+    from moeva2_amd.config_parser.config_parser import get_config, get_dict_hash
+    from moeva2_amd.experiments.united.moeva_run import run
+
+    cfg_dir = os.path.join(os.path.dirname(RES), "config")
+    c = get_config(["-c", f"{cfg_dir}/rq4.lcld.moeva_augmented.yaml", "-p", "budget=3",
+                    "-p", "n_initial_state=4", "-p", f"dirs.results={tmp_path}",
+                    "-j", '{"reconstruction":true,"save_history":"reduced",'
+                          '"paths":{"important_features":"./data/lcld/important_features.npy"}}'])
+    m = run(c, verbose=False)
+    xa = np.load(tmp_path / f"x_attacks_moeva_{get_dict_hash(c)}.npy")
+    assert xa.shape == (4, 203, 57)
+    # reconstructed XOR columns agree with augment_data of the base columns
+    from moeva2_amd.examples.utils import augment_data
+
+    imp = np.load(os.path.join(RES, "data/lcld/important_features.npy"))
+    np.testing.assert_array_equal(xa, augment_data(xa[..., :47], imp))
+    assert 0.0 <= m["objectives_list"][0]["o7"] <= 1.0
