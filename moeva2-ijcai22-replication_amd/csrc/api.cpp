@@ -87,6 +87,8 @@ struct mv_engine {
   bool attack_ready = false;
   bool has_model = false;
   long long* d_phase = nullptr;  // MV_SURV_PHASES=1: survival phase clocks [B][16]
+  unsigned long long* dom_g = nullptr;  // P + O > SURV_NLDS: survival dominance bitsets
+  size_t dom_stride = 0;
   float* xml = nullptr;  // k_vary -> k_mlp scratch
   size_t xml_cap = 0;
   hipError_t ensure_xml(size_t rows) {
@@ -489,7 +491,9 @@ int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t
   if (B <= 0 || N <= 0 || N > SURV_NMAX || R <= 0 || R > SURV_RMAX || n_survive <= 0 ||
       n_survive > N || !F || !ref_points || !ideal || !worst || !extreme || !has_extreme ||
       !survivors)
-    return fail(MV_ERR_ARG, "bad mv_survive arguments (N <= 512, R <= 640, n_survive <= N)");
+    return fail(MV_ERR_ARG, "bad mv_survive arguments (N <= 1024, R <= 640, n_survive <= N)");
+  if (surv_lds_bytes(N, R, 1) > 160 * 1024)
+    return fail(MV_ERR_ARG, "mv_survive: N and R too large for the survival LDS workspace");
   SurvArgs a{};
   a.N = N;
   a.n_survive = n_survive;
@@ -510,7 +514,13 @@ int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t
   a.niche = niche;
   a.dist = dist;
   a.nadir = nadir;
-  HIPCHK(launch_survive(a, B, (hipStream_t)stream));
+  if (N > SURV_NLDS) {  // dominance bitsets in HBM, stream-ordered scratch
+    a.dom_stride = (size_t)N * ((N + 63) / 64);
+    HIPCHK(hipMallocAsync((void**)&a.dom_g, (size_t)B * a.dom_stride * 8, (hipStream_t)stream));
+  }
+  const hipError_t le = launch_survive(a, B, (hipStream_t)stream);
+  if (a.dom_g) HIPCHK(hipFreeAsync(a.dom_g, (hipStream_t)stream));
+  HIPCHK(le);
   return MV_OK;
 }
 
@@ -548,8 +558,13 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   if (P < 2 || O < 2 || (O & 1) || G < 1 || R < 1 || R > SURV_RMAX || P + O > SURV_NMAX ||
       !prm->ref_points || prm->history < 0 || prm->history > 2)
     return fail(MV_ERR_ARG,
-                "bad attack parameters (even n_offsprings, pop_size + n_offsprings <= 512, "
+                "bad attack parameters (even n_offsprings, pop_size + n_offsprings <= 1024, "
                 "n_ref <= 640)");
+  {
+    const int n_m = (O + 1) / 2, pslots = ((n_m * 4 + P - 1) / P) * P;
+    if (surv_lds_bytes(P + O, R, pslots) > 160 * 1024)
+      return fail(MV_ERR_ARG, "pop_size + n_offsprings and n_ref too large for the survival LDS");
+  }
   hipStream_t stream = (hipStream_t)stream_;
   HIPCHK(hipSetDevice(e->device));
   const int B = e->B, V = e->p.V, S = P + O;
@@ -572,6 +587,12 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     A(&e->pop_slot, (size_t)B * P);
     A(&e->free_slot, (size_t)B * O);
     A(&e->parents, (size_t)B * O);
+    e->dom_g = nullptr;
+    e->dom_stride = 0;
+    if (S > SURV_NLDS) {
+      e->dom_stride = (size_t)S * ((S + 63) / 64);
+      A(&e->dom_g, (size_t)B * e->dom_stride);
+    }
     A(&e->ideal, (size_t)B * 3);
     A(&e->worst, (size_t)B * 3);
     A(&e->extreme, (size_t)B * 9);
@@ -653,6 +674,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     s.has_extreme += b0;
     if (s.parents_out) s.parents_out += b0 * O;
     if (s.phase) s.phase += b0 * 16;
+    if (s.dom_g) s.dom_g += b0 * s.dom_stride;
     return s;
   };
   // initial population evaluation (pymoo _initialize)
@@ -686,6 +708,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.extreme = e->extreme;
   sa.has_extreme = e->has_ext;
   sa.O_next = O;
+  sa.dom_g = e->dom_g;
+  sa.dom_stride = e->dom_stride;
   if (std::getenv("MV_SURV_PHASES")) {
     if (!e->d_phase) {
       HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 16 * sizeof(long long)));

@@ -22,7 +22,8 @@ constexpr int VARY_T = 256;      // threads per k_gen / k_cons workgroup (4 wave
 constexpr int VARY_ROWS_MAX = 32; // rows of one state per k_gen / k_cons workgroup (swept: 16/32/64)
 constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
-constexpr int SURV_NMAX = 512;   // merged individuals per state handled in LDS
+constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P + O = 963)
+constexpr int SURV_NLDS = 512;   // up to this N the dominance bitsets live in LDS, else in HBM
 constexpr int SURV_RMAX = 640;   // reference points
 constexpr int ARG_SLOTS = 32;    // constant-memory launch-argument slots per device
 constexpr int MAX_GROUPS = 4;    // state groups (streams) of one attack
@@ -139,6 +140,8 @@ struct SurvArgs {
   int O_next;               // offspring of the next generation (selection)
   int sel_gen;
   long long* phase;         // [B][16] clock64() at phase boundaries (development), or NULL
+  unsigned long long* dom_g;  // N > SURV_NLDS: dominance bitsets [B][dom_stride] in HBM
+  size_t dom_stride;
 };
 
 // Stand-alone classifier forward (Classifier.predict_proba) -------------------------------

@@ -74,6 +74,7 @@ struct SurvOff {
 };
 
 __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
+  const bool dom_lds = N <= SURV_NLDS;
   const unsigned NW = (N + 63) / 64;
   const unsigned RN = R + 3;
   SurvOff o;
@@ -88,7 +89,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(dist, (size_t)N * 8)
   TAKE(red, (SURV_T / 64) * 16 * 8)
   TAKE(scal, 32 * 8)
-  TAKE(dom, (size_t)N * NW * 8)
+  TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)
   TAKE(cur, NW * 8)
   TAKE(I, N * 4)
@@ -272,6 +273,9 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
 
 }  // namespace
 
+// NWMAX: dominance words per individual held in registers (N <= 64 NWMAX); above
+// SURV_NLDS the bitsets go to the HBM scratch a.dom_g instead of LDS.
+template <int NWMAX>
 __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -289,7 +293,10 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   L.dist = (double*)(smem + o.dist);
   L.red = (double*)(smem + o.red);
   L.scal = (double*)(smem + o.scal);
-  L.dom = (unsigned long long*)(smem + o.dom);
+  if (NWMAX * 64 > SURV_NLDS)
+    L.dom = a.dom_g + (size_t)b * a.dom_stride;
+  else
+    L.dom = (unsigned long long*)(smem + o.dom);
   L.ranked = (unsigned long long*)(smem + o.ranked);
   L.cur = (unsigned long long*)(smem + o.cur);
   L.I = (int*)(smem + o.I);
@@ -401,7 +408,6 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Lane l keeps the rows
   // i = 64q + l in registers (NaN rows dominate nothing); a wave sweeps j.
   {
-    constexpr int NWMAX = SURV_NMAX / 64;
     double fi[NWMAX][3];
 #pragma unroll
     for (int q = 0; q < NWMAX; ++q) {
@@ -950,12 +956,19 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   const size_t lds = surv_lds_bytes(a.N, a.R, pslots);
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)k_survive, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NMAX / 64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     configured = true;
   }
-  hipLaunchKernelGGL(k_survive, dim3(B), dim3(SURV_T), lds, stream, a);
+  if (a.N <= SURV_NLDS) {
+    hipLaunchKernelGGL(k_survive<SURV_NLDS / 64>, dim3(B), dim3(SURV_T), lds, stream, a);
+  } else {
+    if (!a.dom_g || a.dom_stride < (size_t)a.N * ((a.N + 63) / 64)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_survive<SURV_NMAX / 64>, dim3(B), dim3(SURV_T), lds, stream, a);
+  }
   return hipGetLastError();
 }
 

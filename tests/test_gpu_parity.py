@@ -134,13 +134,15 @@ def _run_survive(F, ref, n_survive, seed, gen, state):
                 nadir=nadir.cpu().numpy())
 
 
-@pytest.mark.parametrize("N,n_survive", [(303, 203), (203, 203), (120, 100)])
+@pytest.mark.parametrize("N,n_survive", [(303, 203), (203, 203), (120, 100), (963, 643),
+                                         (643, 643)])
 def test_survival_bit_exact_vs_oracle(N, n_survive):
+    """N > 512 (Moeva2's default n_pop 640: P + O = 963) keeps the dominance bitsets in HBM."""
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
     rng = np.random.default_rng(N)
     B = 5
-    ref = energy_ref_dirs(3, 200, seed=1)
+    ref = energy_ref_dirs(3, 640 if N > 512 else 200, seed=1)
     asp = np.full((1, 3), 1.0 / 3.0)
     state = dict(ideal=np.full((B, 3), np.inf), worst=np.full((B, 3), -np.inf),
                  extreme=np.zeros((B, 9)), has=np.zeros(B, np.int32))
@@ -535,3 +537,36 @@ def test_moeva_driver_augmented_reconstruction(tmp_path):
     imp = np.load(os.path.join(RES, "data/lcld/important_features.npy"))
     np.testing.assert_array_equal(xa, augment_data(xa[..., :47], imp))
     assert 0.0 <= m["objectives_list"][0]["o7"] <= 1.0
+
+
+def test_attack_default_population_640(monkeypatch):
+    """Moeva2's default n_pop 640 / n_offsprings 320 (moeva2.py:44-46): survival on the
+    objective arrays of the oracle's attack is bit-exact, the device attack keeps its
+    invariants and does not depend on the state grouping (HBM dominance scratch offsets)."""
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    p = Project("lcld")
+    B, G, P, O, seed = 2, 3, 643, 320, 5
+    ref = energy_ref_dirs(3, 640, seed=1)
+    asp = np.full((1, 3), 1.0 / 3.0)
+    seqs = [_oracle_attack_merges(p.problem(p.x[b]), ref, G, P, O, seed) for b in range(B)]
+    state = dict(ideal=np.full((B, 3), np.inf), worst=np.full((B, 3), -np.inf),
+                 extreme=np.zeros((B, 9)), has=np.zeros(B, np.int32))
+    ost = [mo.SurvivalState() for _ in range(B)]
+    for gen in range(G):
+        F = np.stack([s[gen] for s in seqs])
+        got = _run_survive(F, ref, P, seed, gen, state)
+        for b in range(B):
+            r = mo.survive(F[b], P, ost[b], ref, asp, 0.05, seed, gen)
+            np.testing.assert_array_equal(got["surv"][b], r.survivors, f"gen {gen} state {b}")
+    X = p.x[:5]
+    monkeypatch.setenv("MV_GROUPS", "1")
+    eng, g1, F1, _, _ = _attack("lcld", X, 4, 9, P=P, O=O)
+    monkeypatch.setenv("MV_GROUPS", "4")
+    _, g4, F4, _, _ = _attack("lcld", X, 4, 9, P=P, O=O)
+    np.testing.assert_array_equal(g1.cpu().numpy(), g4.cpu().numpy())
+    np.testing.assert_array_equal(F1.cpu().numpy(), F4.cpu().numpy())
+    F2 = torch.empty_like(F1)
+    eng.evaluate(g1, F2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(F2.cpu().numpy(), F1.cpu().numpy())
