@@ -39,7 +39,52 @@ WORKLOADS = {
                             scaler="models/lcld/scaler.npz",
                             x="data/lcld/x_candidates_synthetic.npy", n_pop=200, n_off=100,
                             n_gen=100, norm=2, history="full", n_states=64),
+    # BASELINE.json configs[2]: LCLD vs the augmented (robust) model, full state set, 1 GPU
+    "rq4.lcld.moeva_augmented": dict(project="lcld_augmented",
+                                     features="data/lcld/features_augmented.csv",
+                                     constraints="data/lcld/constraints_augmented.csv",
+                                     model="models/lcld/nn_augmented_moeva_best.npz",
+                                     scaler="models/lcld/scaler_augmented.npz",
+                                     x="data/lcld/x_candidates_synthetic_augmented.npy",
+                                     n_pop=200, n_off=100, n_gen=100, norm=2, history="full"),
+    # configs[3]: synthetic scale-out, LCLD-shaped states x Moeva2's default n_pop 640
+    "synthetic.lcld.scaleout": dict(project="lcld", features="data/lcld/features.csv",
+                                    constraints="data/lcld/constraints.csv",
+                                    model="models/lcld/nn.npz", scaler="models/lcld/scaler.npz",
+                                    x="data/lcld/x_candidates_synthetic.npy", n_pop=640,
+                                    n_off=320, n_gen=100, norm=2, history="False",
+                                    n_states=100000),
+    # configs[4]: botnet-shaped 756-feature workload, wider 4-layer MLP (random init, seed 7),
+    # 10k states x 100 offspring = 1M candidates per generation
+    "synthetic.botnet.wide": dict(project="botnet", features="data/botnet/features.csv",
+                                  constraints="data/botnet/constraints.csv",
+                                  model="synthetic:756-512-512-256-2:7",
+                                  scaler="models/botnet/scaler.npz",
+                                  x="data/botnet/x_candidates_common.npy", n_pop=200, n_off=100,
+                                  n_gen=100, norm=2, history="False", n_states=10000),
 }
+
+
+def synthetic_mlp(spec):
+    """'synthetic:d0-d1-...:seed' -> Dense relu..softmax weights ~ N(0, 1/fan_in)."""
+    from moeva2_amd.io.tf_bundle import DenseMLP
+
+    _, dims, seed = spec.split(":")
+    dims = [int(d) for d in dims.split("-")]
+    rng = np.random.default_rng(int(seed))
+    W = [(rng.standard_normal((a, b)) / np.sqrt(a)).astype(np.float32)
+         for a, b in zip(dims[:-1], dims[1:])]
+    bs = [np.zeros(b, np.float32) for b in dims[1:]]
+    return DenseMLP(W, bs, ["relu"] * (len(dims) - 2) + ["softmax"])
+
+
+def load_states(w):
+    """The workload's initial states; synthetic scale-outs tile the shipped set."""
+    X = np.load(os.path.join(RES, w["x"]), allow_pickle=False)
+    n = w.get("n_states")
+    if n is not None:
+        X = X[:n] if n <= X.shape[0] else np.resize(X, (n, X.shape[1]))
+    return np.ascontiguousarray(X)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector peak)
@@ -66,7 +111,12 @@ def build_engine(w, device):
 
     c = get_constraints_from_str(w["project"])(os.path.join(RES, w["features"]),
                                                os.path.join(RES, w["constraints"]))
-    clf = Classifier(load_model(os.path.join(RES, w["model"])))
+    if w["model"].startswith("synthetic:"):
+        from moeva2_amd.attacks.moeva2.classifier import DenseMLPModel
+
+        clf = Classifier(DenseMLPModel(synthetic_mlp(w["model"])))
+    else:
+        clf = Classifier(load_model(os.path.join(RES, w["model"])))
     eng = get_engine(c, clf, NpScaler(os.path.join(RES, w["scaler"])), w["norm"], True, device)
     return eng, c
 
@@ -96,6 +146,17 @@ def cpu_baseline(w, sample_states=1, sample_gens=100):
             "sample": f"{sample_states} {w['project']} state(s) x {sample_gens} generations "
                       f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack, numpy, 1 process",
             "seconds": dt}
+
+
+def data_note(w, B):
+    src = {"botnet": "reference CTU-13 botnet x_candidates_common.npy",
+           "lcld": "synthetic valid LCLD states (tools/make_synthetic_lcld.py)",
+           "lcld_augmented": "synthetic valid LCLD states + augment_data XOR features"}
+    n_file = np.load(os.path.join(RES, w["x"]), mmap_mode="r").shape[0]
+    how = f"{B} states" + (f", the {n_file} shipped states tiled" if B > n_file else "")
+    clf = ("random-init Dense MLP " + w["model"].split(":")[1]
+           if w["model"].startswith("synthetic:") else "shipped classifier weights")
+    return f"{src[w['project']]} ({how}) + {clf} and shipped scaler"
 
 
 def main():
@@ -135,9 +196,7 @@ def main():
 
     t_load = time.perf_counter()
     eng, c = build_engine(w, device)
-    X = np.load(os.path.join(RES, w["x"]))
-    if "n_states" in w:
-        X = X[: w["n_states"]]
+    X = load_states(w)
     B = X.shape[0]
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
@@ -252,9 +311,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"reference CTU-13 botnet x_candidates_common.npy ({B} states) + shipped "
-                "classifier weights and scaler" if w["project"] == "botnet" else
-                f"synthetic valid LCLD states ({B}) + shipped classifier weights and scaler",
+        "data": data_note(w, B),
         "config": {"workload": args.workload, "states_per_gpu": B, "pop_size": P,
                    "n_offsprings": O, "n_gen": G, "norm": w["norm"], "history": w["history"],
                    "evals_per_state": evals_per_state, "classifier_dtype": "f32 (MFMA)",
@@ -266,7 +323,8 @@ def main():
         "kernels_avg_ms_per_generation": {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms,
                                           "k_survive": surv_ms, "dominant": dom},
     }
-    if rank == 0 and not args.no_cpu_baseline and world == 1:
+    if rank == 0 and not args.no_cpu_baseline and world == 1 and \
+            not w["model"].startswith("synthetic:"):
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_states, args.cpu_gens)
     if rank == 0:
         print(json.dumps(result), flush=True)

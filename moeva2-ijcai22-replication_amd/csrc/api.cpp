@@ -356,10 +356,9 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   if (md) {
     int hmax = 16;
     for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
+    // the attack's classifier tiles (k_mlp / k_mlp2) read the mutable features only
     const size_t lds = mlp_lds_bytes(p.Dm4, hmax, p.dims[p.n_layers - 1], p.dims[p.n_layers]);
-    const size_t lds_pred = mlp_lds_bytes((D + 3) & ~3, hmax, p.dims[p.n_layers - 1],
-                                          p.dims[p.n_layers]);
-    if (lds > 160 * 1024 || lds_pred > 160 * 1024) {
+    if (lds > 160 * 1024) {
       delete e;
       return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
     }
