@@ -401,11 +401,21 @@ __device__ __forceinline__ void glds_copy(unsigned char* lds, const unsigned cha
 struct RowChunk {
   int b, i0, i1, nrw;
 };
+// XCD-aware order: the dispatcher deals workgroup i to XCD i mod 8, so logical chunk ids
+// are renumbered to keep consecutive ones -- the chunks of one state, which read the same
+// parents and state blob -- on one XCD and its L2.
+__device__ __forceinline__ int xcd_local_id() {
+  constexpr int NX = 8;
+  const int G = gridDim.x, i = blockIdx.x;
+  const int q = G / NX, r = G % NX, x = i % NX, k = i / NX;
+  return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
 __device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
   RowChunk r;
   const int nchunk = (n + rows_wg - 1) / rows_wg;
-  r.b = blockIdx.x / nchunk;
-  r.i0 = (blockIdx.x - r.b * nchunk) * rows_wg;
+  const int id = xcd_local_id();
+  r.b = id / nchunk;
+  r.i0 = (id - r.b * nchunk) * rows_wg;
   r.i1 = min(n, r.i0 + rows_wg);
   const int span = r.i1 - r.i0 - wave;
   r.nrw = span > 0 ? (span + 3) / 4 : 0;
