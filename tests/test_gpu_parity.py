@@ -570,3 +570,38 @@ def test_attack_default_population_640(monkeypatch):
     eng.evaluate(g1, F2)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(F2.cpu().numpy(), F1.cpu().numpy())
+
+
+def test_success_rate_matches_oracle_attack_botnet():
+    """The headline config's shape (botnet, P = 203, O = 100, L2, eps 4, thr 0.5): device
+    attack vs the oracle's CPU attack on the same shipped states, budget and seed; o1..o7
+    within max(1 pp, one state)."""
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    p = Project("botnet")
+    B, G, P, O, seed = 12, 100, 203, 100, 3
+    X = p.x[:B]
+    _, g, _, _, ref = _attack("botnet", X, G, seed, P=P, O=O)
+    np.testing.assert_array_equal(ref, energy_ref_dirs(3, 200, seed=1))
+    genes = g.cpu().numpy()
+    sc, mn = p.ml
+
+    def fn(xi, xs):
+        return mo.objectives_calc(xi, xs, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, 2)
+
+    x_dev, x_cpu = [], []
+    for b in range(B):
+        r = mo.run_attack(p.problem(X[b]), ref, G, P, O, seed)
+        x_cpu.append(mo.genetic_to_ml(p.lay, r.pop_X, X[b]))
+        x_dev.append(mo.genetic_to_ml(p.lay, genes[b], X[b]))
+    sr_dev = mo.success_rate_3d(X, x_dev, fn, 0.5, 4)
+    sr_cpu = mo.success_rate_3d(X, x_cpu, fn, 0.5, 4)
+    # at this budget few botnet states flip (the reference runs 1000 generations), so also
+    # compare the attack's progress: each state's best f1 in its final population
+    best_dev = np.array([fn(X[b], x_dev[b])[:, 1].min() for b in range(B)])
+    best_cpu = np.array([fn(X[b], x_cpu[b])[:, 1].min() for b in range(B)])
+    print("o1..o7 dev", sr_dev, "cpu", sr_cpu, "best f1 dev", best_dev.mean(), "cpu",
+          best_cpu.mean(), "max |diff|", np.abs(best_dev - best_cpu).max())
+    assert np.all(np.abs(sr_dev - sr_cpu) <= max(0.01, 1.0 / B) + 1e-12), (sr_dev, sr_cpu)
+    assert abs(best_dev.mean() - best_cpu.mean()) <= 0.01, (best_dev, best_cpu)
