@@ -136,12 +136,6 @@ __device__ __forceinline__ bool arg_better(double v, int i, double bv, int bi) {
   return v < bv || (v == bv && i < bi);
 }
 
-__device__ __forceinline__ bool dominates(const double* a, const double* b) {
-  const bool lt = (a[0] < b[0]) | (a[1] < b[1]) | (a[2] < b[2]);
-  const bool gt = (a[0] > b[0]) | (a[1] > b[1]) | (a[2] > b[2]);
-  return lt && !gt;
-}
-
 // Ordered stream compaction of the indices i in [0, n) with pred(i) into out[base..].
 // Returns the count (uniform).  Uses red scratch as int[4+1].
 template <class Pred>
@@ -405,28 +399,55 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   }
   PHASE(11)
 
-  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Lane l keeps the rows
-  // i = 64q + l in registers (NaN rows dominate nothing); a wave sweeps j.
+  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the
+  // unordered 64x64 block pairs (qi <= qj) split into two 32-row halves of block qj; lane
+  // l holds row i = 64 qi + l (NaN past N: dominates nothing).  One pass of the six
+  // compares per (i, j) gives both directions: lt && !gt -> i dominates j (ballot = word qi
+  // of dom[j]); gt && !lt -> j dominates i, gathered per lane into the 32-bit half h of word
+  // qj of dom[i] (off-diagonal pairs only; the diagonal block is covered by its ballots).
   {
-    double fi[NWMAX][3];
-#pragma unroll
-    for (int q = 0; q < NWMAX; ++q) {
-      const int i = q * 64 + lane;
-      const bool ok = q < NW && i < N;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) fi[q][k] = ok ? L.F[i * 3 + k] : __builtin_nan("");
-    }
-    for (int j = wave; j < N; j += SURV_T / 64) {
-      const double fj[3] = {L.F[j * 3], L.F[j * 3 + 1], L.F[j * 3 + 2]};
+    unsigned* dom32 = (unsigned*)L.dom;
+    const int n_items = NW * (NW + 1);
+    for (int t = wave; t < n_items; t += SURV_T / 64) {
+      const int h = t & 1;
+      int qi = 0, rem = t >> 1;
+      while (rem >= NW - qi) {
+        rem -= NW - qi;
+        ++qi;
+      }
+      const int qj = qi + rem;
+      const int i = qi * 64 + lane;
+      const bool ok = i < N;
+      const double fi0 = ok ? L.F[i * 3 + 0] : __builtin_nan("");
+      const double fi1 = ok ? L.F[i * 3 + 1] : __builtin_nan("");
+      const double fi2 = ok ? L.F[i * 3 + 2] : __builtin_nan("");
+      const int j0 = qj * 64 + h * 32;
+      const int jn = min(32, N - j0);
+      // four independent rows per step (the step is latency-bound: LDS broadcast ->
+      // compares -> ballot); lane jj keeps the ballot of row j0 + jj until the item ends
+      unsigned acc = 0u;
       unsigned long long mine = 0ull;
+      for (int jj = 0; jj < jn; jj += 4) {
+        double g[4][3];
 #pragma unroll
-      for (int q = 0; q < NWMAX; ++q) {
-        if (q < NW) {
-          const unsigned long long msk = __ballot(dominates(fi[q], fj));
-          if (lane == q) mine = msk;
+        for (int u = 0; u < 4; ++u) {
+          const int j = min(j0 + jj + u, N - 1);
+          g[u][0] = L.F[j * 3];
+          g[u][1] = L.F[j * 3 + 1];
+          g[u][2] = L.F[j * 3 + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool valid = jj + u < jn;
+          const bool lt = (fi0 < g[u][0]) | (fi1 < g[u][1]) | (fi2 < g[u][2]);
+          const bool gt = (fi0 > g[u][0]) | (fi1 > g[u][1]) | (fi2 > g[u][2]);
+          const unsigned long long m = __ballot(valid && lt && !gt);
+          if (lane == jj + u) mine = m;
+          acc |= (valid && gt && !lt) ? (1u << ((jj + u) & 31)) : 0u;
         }
       }
-      if (lane < NW) L.dom[(size_t)j * NW + lane] = mine;
+      if (lane < jn) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
+      if (qi != qj && ok) dom32[((size_t)i * NW + qj) * 2 + h] = acc;
     }
   }
   __syncthreads();
@@ -671,17 +692,19 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
-      // fp32 pre-filter of the squared perpendicular distances.  Its error is below
-      // 4e-6 |N|^2, so only directions whose fp32 value is within tol = 3e-5 (|N|^2 + best)
-      // of the fp32 minimum can hold the fp64 minimum: those few get the exact fp64
-      // distance and np.argmin's order (first index among equal sqrt'ed distances).  A NaN
-      // or overflow sends the individual to the full exact pass below.
+      // fp32 pre-filter of the squared perpendicular distances, as |N|^2 - (N.u)^2 for the
+      // unit directions u (3 FMAs + 1 per direction).  Its error is below 2e-6 |N|^2
+      // (dot product 3.1e-7 |N|, rounding of u to fp32 1.2e-7, |N|^2 1.8e-7, all relative),
+      // so only directions whose fp32 value is within tol = 3e-5 (|N|^2 + best) of the fp32
+      // minimum can hold the fp64 minimum: those few get the exact fp64 distance and
+      // np.argmin's order (first index among equal sqrt'ed distances).  A NaN or overflow
+      // sends the individual to the full exact pass below.
       const float n0 = (float)Nn[0], n1 = (float)Nn[1], n2 = (float)Nn[2];
+      const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
       auto d2f = [&](int j) {
         const float4 u = L.Uf[j];
         const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
-        const float e0 = fmaf(sp, u.x, -n0), e1 = fmaf(sp, u.y, -n1), e2 = fmaf(sp, u.z, -n2);
-        return fmaf(e0, e0, fmaf(e1, e1, e2 * e2));
+        return fmaf(-sp, sp, nn);
       };
       if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
           !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0
@@ -699,7 +722,6 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       }
       for (; j < RN; ++j) b0 = fminf(b0, d2f(j));
       const float best = fminf(fminf(b0, b1), fminf(b2, b3));
-      const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
       const float lim = best + 3e-5f * (nn + best);
       if (lim < __builtin_inff()) {  // false on NaN / inf
         double bd = __builtin_inf();
