@@ -688,7 +688,15 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       den[k] = nadir[k] - ideal[k];
       if (den[k] == 0.0) den[k] = 1e-12;
     }
-    for (int p = tid; p < n_ranked; p += SURV_T) {
+    // Two adjacent lanes per individual, each sweeping half of the directions (N = P + O
+    // individuals on 8 waves would otherwise leave 3 waves idle and double up one SIMD);
+    // the halves combine with lane swaps: fp32 minimum (exact), then the fp64 candidate
+    // minimum in np.argmin's order (arg_better is a total order, so the combination equals
+    // the sequential scan).
+    const int jmid = RN / 2;
+    for (int v = tid; v < 2 * n_ranked; v += SURV_T) {
+      const int p = v >> 1, hf = v & 1;
+      const int jlo = hf ? jmid : 0, jhi = hf ? RN : jmid;
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
@@ -707,23 +715,26 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
         return fmaf(-sp, sp, nn);
       };
       if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
-          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0
-        L.niche[p] = 0;
-        L.dist[p] = 0.0;
+          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0 (both lanes)
+        if (!hf) {
+          L.niche[p] = 0;
+          L.dist[p] = 0.0;
+        }
         continue;
       }
       float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;  // 4 independent chains
-      int j = 0;
-      for (; j + 4 <= RN; j += 4) {
+      int j = jlo;
+      for (; j + 4 <= jhi; j += 4) {
         b0 = fminf(b0, d2f(j));
         b1 = fminf(b1, d2f(j + 1));
         b2 = fminf(b2, d2f(j + 2));
         b3 = fminf(b3, d2f(j + 3));
       }
-      for (; j < RN; ++j) b0 = fminf(b0, d2f(j));
-      const float best = fminf(fminf(b0, b1), fminf(b2, b3));
+      for (; j < jhi; ++j) b0 = fminf(b0, d2f(j));
+      float best = fminf(fminf(b0, b1), fminf(b2, b3));
+      best = fminf(best, __shfl_xor(best, 1, 64));
       const float lim = best + 3e-5f * (nn + best);
-      if (lim < __builtin_inff()) {  // false on NaN / inf
+      if (lim < __builtin_inff()) {  // false on NaN / inf (the same in both lanes)
         double bd = __builtin_inf();
         int bj = 0;
         auto cand = [&](int j) {  // exact fp64 distance, np.argmin order
@@ -736,19 +747,27 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
             bj = j;
           }
         };
-        int j = 0;
-        for (; j + 4 <= RN; j += 4) {  // rare beyond the minimum itself
+        int j = jlo;
+        for (; j + 4 <= jhi; j += 4) {  // rare beyond the minimum itself
           const float d0 = d2f(j), d1 = d2f(j + 1), d2 = d2f(j + 2), d3 = d2f(j + 3);
           if (d0 <= lim) cand(j);
           if (d1 <= lim) cand(j + 1);
           if (d2 <= lim) cand(j + 2);
           if (d3 <= lim) cand(j + 3);
         }
-        for (; j < RN; ++j)
+        for (; j < jhi; ++j)
           if (d2f(j) <= lim) cand(j);
-        L.niche[p] = bj;
-        L.dist[p] = bd;
-      } else {
+        const double od = __shfl_xor(bd, 1, 64);
+        const int oj = __shfl_xor(bj, 1, 64);
+        if (arg_better(od, oj, bd, bj)) {
+          bd = od;
+          bj = oj;
+        }
+        if (!hf) {
+          L.niche[p] = bj;
+          L.dist[p] = bd;
+        }
+      } else if (!hf) {
         L.key[atomicAdd(&L.iscal[15], 1)] = p;
       }
     }
