@@ -135,9 +135,11 @@ def _run_survive(F, ref, n_survive, seed, gen, state):
 
 
 @pytest.mark.parametrize("N,n_survive", [(303, 203), (203, 203), (120, 100), (963, 643),
-                                         (643, 643)])
+                                         (643, 643), (64, 40), (96, 64), (33, 20)])
 def test_survival_bit_exact_vs_oracle(N, n_survive):
-    """N > 512 (Moeva2's default n_pop 640: P + O = 963) keeps the dominance bitsets in HBM."""
+    """N > 512 (Moeva2's default n_pop 640: P + O = 963) keeps the dominance bitsets in HBM.
+    N = 64, 96, 33 hit the dominance block-pair edges (a full last block, a last block of
+    exactly one 32-row half, a one-row second half)."""
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
     rng = np.random.default_rng(N)
