@@ -31,7 +31,7 @@ struct SurvLds {
   float4* Uf;       // [R+3] the same in fp32 (association pre-filter)
   double* dist;     // [N]
   double* red;      // [waves*16] reduction scratch
-  double* scal;     // [32] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9)
+  double* scal;     // [40] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9) prev ext(9)
   unsigned long long* dom;     // [N*NW]
   unsigned long long* ranked;  // [NW]
   unsigned long long* cur;     // [NW]
@@ -88,7 +88,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(Uf, (size_t)RN * 16)
   TAKE(dist, (size_t)N * 8)
   TAKE(red, (SURV_T / 64) * 16 * 8)
-  TAKE(scal, 32 * 8)
+  TAKE(scal, 40 * 8)
   TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)
   TAKE(cur, NW * 8)
@@ -320,6 +320,11 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
   double* wfront = L.scal + 9;
   double* nadir = L.scal + 12;
   double* ext = L.scal + 15;  // 9
+  double* pext = L.scal + 24;  // 9: the carried extremes, staged at entry
+  const int has_ext = a.has_extreme[b] != 0;
+  // carried ideal / worst, loaded at entry so their latency overlaps the F load
+  const double pre_ideal = tid < 3 ? a.ideal[(size_t)b * 3 + tid] : 0.0;
+  const double pre_worst = tid < 3 ? a.worst[(size_t)b * 3 + tid] : 0.0;
   const bool slot_mode = a.pop_slot != nullptr;
 #define PHASE(k) \
   if (a.phase && tid == 0) a.phase[(size_t)b * 16 + (k)] = clock64();
@@ -343,6 +348,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     L.sel[m] = 0;
   }
   for (int r = tid; r < R * 3; r += SURV_T) L.ref[r] = a.ref[r];
+  if (tid < 9) pext[tid] = a.extreme[(size_t)b * 9 + tid];
   for (int q = tid; q < NW; q += SURV_T) {
     L.ranked[q] = 0ull;
     L.cur[q] = 0ull;
@@ -385,7 +391,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     __syncthreads();
     if (tid < 3) {
       const int k = tid;
-      double vmn = a.ideal[(size_t)b * 3 + k], vmx = a.worst[(size_t)b * 3 + k];
+      double vmn = pre_ideal, vmx = pre_worst;
       double vwp = -__builtin_inf();
       for (int w = 0; w < SURV_T / 64; ++w) {
         vmn = min_prop(vmn, L.red[w * 16 + k]);
@@ -526,8 +532,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
 
   // ---- extreme points (ASF over prev extremes + front 0 + ref points), worst of front
   {
-    const int has = a.has_extreme[b] != 0;
-    const int ne = has ? 3 : 0;
+    const int ne = has_ext ? 3 : 0;
     const int ncand = ne + n0 + R;
     double bv[3];
     int bi[3];
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     for (int c = tid; c < ncand; c += SURV_T) {
       double row[3];
       if (c < ne) {
-        for (int k = 0; k < 3; ++k) row[k] = a.extreme[(size_t)b * 9 + c * 3 + k];
+        for (int k = 0; k < 3; ++k) row[k] = pext[c * 3 + k];
       } else if (c < ne + n0) {
         const int m = L.I[c - ne];
         for (int k = 0; k < 3; ++k) {
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
         wfront[i] = w;
         double row[3];
         if (ix < ne) {
-          for (int k = 0; k < 3; ++k) row[k] = a.extreme[(size_t)b * 9 + ix * 3 + k];
+          for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
         } else if (ix < ne + n0) {
           const int m = L.I[ix - ne];
           for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
