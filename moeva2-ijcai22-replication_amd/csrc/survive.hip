@@ -752,16 +752,33 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
             bj = j;
           }
         };
-        int j = jlo;
-        for (; j + 4 <= jhi; j += 4) {  // rare beyond the minimum itself
-          const float d0 = d2f(j), d1 = d2f(j + 1), d2 = d2f(j + 2), d3 = d2f(j + 3);
-          if (d0 <= lim) cand(j);
-          if (d1 <= lim) cand(j + 1);
-          if (d2 <= lim) cand(j + 2);
-          if (d3 <= lim) cand(j + 3);
+        // second sweep only over the chains whose minimum is within lim (usually just the
+        // chain holding the minimum): chain u = jlo + u + 4k, chain 0 also takes the tail.
+        // d2f is the same expression as in the first sweep, so no candidate is missed, and
+        // arg_better is a total order, so the visiting order does not change the result.
+        const int n4 = (jhi - jlo) >> 2;
+        unsigned cm = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) | (b2 <= lim ? 4u : 0u) |
+                      (b3 <= lim ? 8u : 0u);
+        while (cm) {
+          const int u = __builtin_ctz(cm);
+          cm &= cm - 1u;
+          int k = 0;
+          for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
+            const int jc = jlo + 4 * k + u;
+            const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
+            if (d0 <= lim) cand(jc);
+            if (d1 <= lim) cand(jc + 4);
+            if (d2 <= lim) cand(jc + 8);
+            if (d3 <= lim) cand(jc + 12);
+          }
+          for (; k < n4; ++k) {
+            const int jc = jlo + 4 * k + u;
+            if (d2f(jc) <= lim) cand(jc);
+          }
+          if (u == 0)
+            for (int jc = jlo + 4 * n4; jc < jhi; ++jc)
+              if (d2f(jc) <= lim) cand(jc);
         }
-        for (; j < jhi; ++j)
-          if (d2f(j) <= lim) cand(j);
         const double od = __shfl_xor(bd, 1, 64);
         const int oj = __shfl_xor(bj, 1, 64);
         if (arg_better(od, oj, bd, bj)) {
