@@ -845,11 +845,15 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     const int* nich = L.niche + fs;
     const double* dst = L.dist + fs;
     const int nlev = N + Lc + 1;
+    int* fill = L.ckey;  // [RN] fill counters of the niche member lists
+    int* mem = L.key;    // [Lc] last-front members grouped by niche (order inside a niche
+                         // is arbitrary: only counts are taken over it)
     for (int n = tid; n < RN; n += SURV_T) {
       cnt[n] = 0;
       mcnt[n] = 0;
       L.dmin[n] = ~0ull;
       bestkr[n] = INT_MAX;
+      fill[n] = 0;
     }
     for (int l = tid; l < nlev; l += SURV_T) L.lround[l] = 0;
     unsigned long long* sk = L.sortk;
@@ -862,11 +866,7 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     }
     __syncthreads();
     for (int p = tid; p < Lc; p += SURV_T) {
-      const unsigned long long kp = sk[p];
-      int r = 0;
-      for (int q = 0; q < Lc; ++q) r += sk[q] < kp ? 1 : 0;
       const int np_ = nich[p];
-      grank[p] = r;
       if (cnt[np_] == 0)
         atomicMin(&L.dmin[np_], (unsigned long long)__double_as_longlong(dst[p]));
     }
@@ -875,8 +875,25 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     block_scan_excl(start, RN, wsum);
     for (int p = tid; p < Lc; p += SURV_T) {
       const int np_ = nich[p];
+      mem[start[np_] + atomicAdd(&fill[np_], 1)] = p;
+    }
+    __syncthreads();
+    // grank = rank of sk[p] among all keys = members of smaller niches (start) + rank inside
+    // its own niche, counted over that niche's members only
+    for (int p = tid; p < Lc; p += SURV_T) {
+      const int np_ = nich[p];
+      const unsigned long long kp = sk[p];
+      int r = 0, t = start[np_];
+      const int te = t + mcnt[np_];
+      for (; t + 4 <= te; t += 4) {  // crowded niches: four gathers in flight
+        const int m0 = mem[t], m1 = mem[t + 1], m2 = mem[t + 2], m3 = mem[t + 3];
+        r += (sk[m0] < kp ? 1 : 0) + (sk[m1] < kp ? 1 : 0) + (sk[m2] < kp ? 1 : 0) +
+             (sk[m3] < kp ? 1 : 0);
+      }
+      for (; t < te; ++t) r += sk[mem[t]] < kp ? 1 : 0;
+      grank[p] = start[np_] + r;
       if (cnt[np_] == 0 && (unsigned long long)__double_as_longlong(dst[p]) == L.dmin[np_])
-        atomicMin(&bestkr[np_], grank[p] - start[np_]);
+        atomicMin(&bestkr[np_], r);
     }
     __syncthreads();
     for (int p = tid; p < Lc; p += SURV_T) {
