@@ -862,7 +862,8 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
     for (int p = tid; p < Lc; p += SURV_T) {
       const unsigned key = rng.draw((uint32_t)p, (uint32_t)a.gen, TAG_NICHE_MEMBER).x;
       atomicAdd(&mcnt[nich[p]], 1);
-      sk[p] = ((unsigned long long)nich[p] << 41) | ((unsigned long long)key << 9) | (unsigned)p;
+      // (niche, member key, position); positions take 10 bits (N <= 1024)
+      sk[p] = ((unsigned long long)nich[p] << 42) | ((unsigned long long)key << 10) | (unsigned)p;
     }
     __syncthreads();
     for (int p = tid; p < Lc; p += SURV_T) {
@@ -913,8 +914,10 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
       const int l = lev[p];
       const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)a.gen,
                                    TAG_NICHE_PERM).x;
-      sk[p] = ((unsigned long long)l << 51) | ((unsigned long long)kr << 19) |
-              ((unsigned long long)nich[p] << 9) | (unsigned)p;
+      // (level, round key, niche) is unique per member (a niche picks at most once per
+      // level), so no position field is needed: niche 11 bits, round key 32, level 21
+      sk[p] = ((unsigned long long)l << 43) | ((unsigned long long)kr << 11) |
+              (unsigned long long)nich[p];
     }
     __syncthreads();
     for (int p = tid; p < Lc; p += SURV_T) {
