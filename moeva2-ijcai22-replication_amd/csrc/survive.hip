@@ -583,8 +583,9 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
         L.red[wave * 16 + 6 + i] = wf[i];
       }
     __syncthreads();
-    if (tid == 0) {
-      for (int i = 0; i < 3; ++i) {
+    if (tid < 3) {  // one thread per objective: winner of the extreme-point argmin
+      {
+        const int i = tid;
         double v = L.red[i];
         int ix = (int)L.red[3 + i];
         double w = L.red[6 + i];
@@ -609,6 +610,9 @@ __global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
         }
         for (int k = 0; k < 3; ++k) ext[i * 3 + k] = row[k];
       }
+    }
+    __syncthreads();
+    if (tid == 0) {
       // nadir (get_nadir_point with the call-site argument swap)
       double M[3][3], plane[3] = {1.0, 1.0, 1.0};
       for (int i = 0; i < 3; ++i)
