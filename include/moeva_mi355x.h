@@ -179,8 +179,17 @@ typedef struct mv_attack_params {
 } mv_attack_params;
 
 /* Whole attack on device: init population + evaluate + (n_gen-1) x {select, vary+evaluate,
- * survive}, no host round trip.  Asynchronous on `stream`. */
+ * survive}, no host round trip.  Asynchronous on `stream`.  Replaces Moeva2.generate's
+ * per-state pymoo.minimize calls (moeva2.py:128-171, 194-205) for ALL bound states.
+ * For the shipped problem layouts it is ONE launch (k_attack: one workgroup per state runs
+ * every generation); other shapes, or attack mode 1, run the per-phase kernel chain
+ * (k_gen, k_cons, k_mlp2, k_survive per generation).  Both give identical results. */
 int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
+/* 0: whole-attack kernel when available (default), 1: per-phase kernel chain. */
+int mv_set_attack_mode(mv_engine* e, int32_t mode);
+/* Device ms of the last profiled mv_attack_run's k_attack launch (0 if the chain ran) and
+ * whether the last run was the whole-attack kernel. */
+int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);
 /* Final population: genes dev [B][P][V], F dev [B][P][3] (either may be NULL). */
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
 /* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */

@@ -83,6 +83,7 @@ struct mv_engine {
   double *ideal = nullptr, *worst = nullptr, *extreme = nullptr;
   int* has_ext = nullptr;
   double* ref = nullptr;
+  std::vector<double> ref_host;  // the reference points currently in e->ref
   double* hist = nullptr;
   bool attack_ready = false;
   bool has_model = false;
@@ -116,6 +117,9 @@ struct mv_engine {
     return err;
   }
   // profiling
+  int attack_mode = 0;      // 0: whole-attack kernel when the shape has an instance, 1: chain
+  bool last_whole = false;  // the last mv_attack_run used the whole-attack kernel
+  hipEvent_t ev_att[2] = {};
   bool profiling = false;
   std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
   int n_var_rec = 0, n_surv_rec = 0;
@@ -145,6 +149,8 @@ struct mv_engine {
     }
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
+    for (auto e : ev_att)
+      if (e) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
 };
@@ -610,8 +616,17 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     e->hist_rows = hist_rows;
     e->attack_ready = true;
   }
-  HIPCHK(hipMemcpy(e->ref, prm->ref_points, (size_t)R * 3 * sizeof(double),
-                   hipMemcpyHostToDevice));
+  // Reference points: a previous attack still queued on another stream may read e->ref,
+  // so they are re-uploaded only when they change, and then behind a device-wide sync.
+  // (Callers pass the same energy directions every time; the common case copies nothing
+  // and keeps the host running ahead of the GPU.)
+  if (realloc || e->ref_host.size() != (size_t)R * 3 ||
+      std::memcmp(e->ref_host.data(), prm->ref_points, (size_t)R * 3 * sizeof(double)) != 0) {
+    HIPCHK(hipDeviceSynchronize());
+    e->ref_host.assign(prm->ref_points, prm->ref_points + (size_t)R * 3);
+    HIPCHK(hipMemcpy(e->ref, e->ref_host.data(), (size_t)R * 3 * sizeof(double),
+                     hipMemcpyHostToDevice));
+  }
   hipLaunchKernelGGL(k_fill_d, dim3(64), dim3(256), 0, stream, e->ideal, (size_t)B * 3,
                      (double)INFINITY);
   hipLaunchKernelGGL(k_fill_d, dim3(64), dim3(256), 0, stream, e->worst, (size_t)B * 3,
@@ -619,6 +634,86 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   hipLaunchKernelGGL(k_fill_i, dim3(64), dim3(256), 0, stream, e->has_ext, (size_t)B, 0);
   HIPCHK(hipGetLastError());
   HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
+  HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
+  const char* env_mode = std::getenv("MV_ATTACK");
+  const bool chain = e->attack_mode == 1 || (env_mode && std::strcmp(env_mode, "chain") == 0);
+  e->last_whole = !chain && attack_supported(e->p, P, O, R);
+  if (e->last_whole) {
+    // the whole GA loop in one launch: one workgroup per state (attack.hip)
+    AttackArgs A{};
+    A.ev = base_rows(e);
+    A.ev.n = P;
+    A.ev.total = B * P;
+    A.ev.mode = 0;
+    A.ev.genes_in = e->pool;
+    A.ev.in_rows = S;
+    A.ev.out_rows = S;
+    A.ev.F = e->poolF;
+    A.ev.hist = prm->history ? e->hist : nullptr;
+    A.ev.hist_rows = hist_rows;
+    A.ev.hist_w = hist_w;
+    A.ev.xml = e->xml;
+    A.ev.xml_rows = P > O ? P : O;  // states run different phases at the same time
+    A.va = base_rows(e);
+    A.va.n = O;
+    A.va.total = B * O;
+    A.va.mode = 1;
+    A.va.genes_in = e->pool;
+    A.va.in_rows = S;
+    A.va.parents = e->parents;
+    A.va.genes_out = e->pool;
+    A.va.out_rows = S;
+    A.va.out_map = e->free_slot;
+    A.va.F = e->poolF;
+    A.va.hist = prm->history ? e->hist : nullptr;
+    A.va.hist_rows = hist_rows;
+    A.va.hist_w = hist_w;
+    A.va.seed = prm->seed;
+    A.va.xml = e->xml;
+    A.va.xml_rows = P > O ? P : O;
+    SurvArgs& s = A.sa;
+    s.n_survive = P;
+    s.P = P;
+    s.O = O;
+    s.F = e->poolF;
+    s.S = S;
+    s.pop_slot = e->pop_slot;
+    s.free_slot = e->free_slot;
+    s.pop_slot_out = e->pop_slot;
+    s.ref = e->ref;
+    s.R = R;
+    s.mu = prm->mu;
+    s.seed = prm->seed;
+    s.ideal = e->ideal;
+    s.worst = e->worst;
+    s.extreme = e->extreme;
+    s.has_extreme = e->has_ext;
+    s.O_next = O;
+    s.dom_g = e->dom_g;
+    s.dom_stride = e->dom_stride;
+    A.parents = e->parents;
+    A.B = B;
+    A.P = P;
+    A.O = O;
+    A.G = G;
+    if (std::getenv("MV_ATT_PROF")) {  // development aid: per-phase clock64 sums per state
+      if (!e->d_phase) {
+        HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 16 * sizeof(long long)));
+        e->attack_allocs.push_back(e->d_phase);
+      }
+      A.prof = e->d_phase;
+    }
+    if (e->profiling) {
+      for (auto& ev : e->ev_att)
+        if (!ev) HIPCHK(hipEventCreate(&ev));
+      HIPCHK(hipEventRecord(e->ev_att[0], stream));
+    }
+    HIPCHK(launch_attack(A, stream));
+    if (e->profiling) HIPCHK(hipEventRecord(e->ev_att[1], stream));
+    e->n_var_rec = 0;
+    e->n_surv_rec = 0;
+    return MV_OK;
+  }
   // Initial states are independent: split them into state groups, each running its own
   // generation chain on its own stream, so one group's latency-bound survival overlaps the
   // other groups' throughput-bound kernels.  Results do not depend on the grouping (every
@@ -687,7 +782,6 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   ev.hist = prm->history ? e->hist : nullptr;
   ev.hist_rows = hist_rows;
   ev.hist_w = hist_w;
-  HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
   ev.xml = e->xml;
   SurvArgs sa{};
   sa.n_survive = P;
@@ -828,6 +922,41 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
     std::fprintf(stderr, " | ideal/worst=%.0f assoc_fast=%.0f flagged=%.1f", red / e->B,
                  afast / e->B, nflag / e->B);
     std::fprintf(stderr, "\n");
+  }
+  return MV_OK;
+}
+
+int mv_set_attack_mode(mv_engine* e, int32_t mode) {
+  if (!e || mode < 0 || mode > 1) return fail(MV_ERR_ARG, "attack mode must be 0 (auto) or 1 (chain)");
+  e->attack_mode = mode;
+  return MV_OK;
+}
+
+int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole) {
+  if (!e) return fail(MV_ERR_ARG, "null engine");
+  if (whole) *whole = e->last_whole ? 1 : 0;
+  if (ms) {
+    *ms = 0.0;
+    if (e->last_whole && e->ev_att[1]) {
+      float t = 0.f;
+      HIPCHK(hipEventSynchronize(e->ev_att[1]));
+      HIPCHK(hipEventElapsedTime(&t, e->ev_att[0], e->ev_att[1]));
+      *ms = t;
+    }
+  }
+  if (e->last_whole && e->d_phase && std::getenv("MV_ATT_PROF") && e->B > 0) {
+    std::vector<long long> ph((size_t)e->B * 16);
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(ph.data(), e->d_phase, (size_t)e->B * 4 * sizeof(long long),
+                     hipMemcpyDeviceToHost));
+    double acc[4] = {0, 0, 0, 0};
+    for (int b = 0; b < e->B; ++b)
+      for (int k = 0; k < 4; ++k) acc[k] += (double)ph[(size_t)b * 4 + k];
+    const double g = e->n_gen > 0 ? e->n_gen : 1;
+    std::fprintf(stderr,
+                 "[mv] k_attack cycles per state-generation: rows %.0f mlp %.0f survive %.0f "
+                 "all %.0f\n", acc[0] / e->B / g, acc[1] / e->B / g, acc[2] / e->B / g,
+                 acc[3] / e->B / g);
   }
   return MV_OK;
 }

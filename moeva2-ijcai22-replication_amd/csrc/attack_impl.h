@@ -1,0 +1,658 @@
+// Whole-attack kernel (gfx950), shared body of attack_ident.hip / attack_ohe.hip: one workgroup per initial state runs the entire MoEvA2 GA
+// loop of Moeva2._one_generate + pymoo.minimize (src/attacks/moeva2/moeva2.py:128-171) --
+// evaluate the initial population, then (n_gen - 1) x {crossover + mutation + evaluation
+// of the offspring, R-NSGA-III survival + the next tournament} -- in ONE launch.
+//
+// Initial states are independent (moeva2.py:194-205), so a state needs no other
+// workgroup's data: its generation chain is a sequence of workgroup phases separated by
+// barriers instead of four kernel launches per generation.  Two workgroups share a CU
+// (LDS <= 80 KiB, <= 128 VGPRs), so one state's latency-bound survival overlaps the other
+// state's HBM / MFMA-bound evaluation on the same CU.
+//
+// Phases (per state, per generation):
+//   rows_state  variation (mode 1) or gene load (mode 0) of the generation's rows, one row per
+//               wave at a time: child genes -> pool, f2 (encoder MinMax distance), the fp32
+//               ML-scaled row -> xml, the ML-space row -> the wave's LDS row buffer ->
+//               constraint program -> f3 (default_problem.py:99-140 minus the classifier).
+//               The child genes are read once (parents) and written once.
+//   mlp_state   the Dense-ReLU chain on v_mfma_f32_16x16x4_f32 over 64-row tiles of the
+//               state's xml rows, final Dense + softmax -> f1 (classifier.py:23-29).
+//   survive_state (survival.h) survival + tournament, state carried in HBM slots.
+// Every phase reuses the per-phase kernels' arithmetic unchanged (rowops.h, survival.h), so
+// the attack is bit-identical to the k_gen/k_cons/k_mlp2/k_survive chain (tested).
+#pragma once
+#include <mutex>
+
+#include "engine.h"
+#include "kernels.h"
+#include "philox.h"
+#include "rowops.h"
+#include "survival.h"
+#include "wave.h"
+
+namespace mv {
+
+// per translation unit: the constant-memory argument ring of this TU's kernels
+static __constant__ AttackArgs c_att[ATT_SLOTS];
+
+namespace {
+struct AttRing {
+  bool ready = false;
+  AttackArgs* host = nullptr;  // pinned [ATT_SLOTS]
+  hipEvent_t ev[ATT_SLOTS] = {};
+  int next = 0;
+};
+constexpr int ATT_MAX_DEV = 64;
+AttRing g_att[ATT_MAX_DEV];
+std::mutex g_att_mu;
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Fused row phase: k_gen + k_cons for the n rows of one state on the workgroup's W waves.
+// Wave w takes rows c0 + w + W k of each chunk of 64 W rows (lane k of the wave holds row
+// k's parents, crossover draws and cached mutations, exactly as k_gen).
+template <bool IDENT, int NT, bool FULL, int T>
+__device__ __forceinline__ void rows_state(const RowsArgs& a, const int b, const int gen,
+                                           const int hist_row0, unsigned char* smem) {
+  constexpr int W = T / 64;
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // uniform by construction; readfirstlane lets the non-inlined phase keep them in SGPRs
+  const int V = __builtin_amdgcn_readfirstlane(p.V);
+  const int Dm = __builtin_amdgcn_readfirstlane(p.Dm);
+  const int Dm4 = __builtin_amdgcn_readfirstlane(p.Dm4);
+  const VaryOff o = vary_offsets(p);
+  const FusedLds L = fused_lds(o, W);
+  const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
+  glds_copy<T>(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
+  glds_copy<T>(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
+  glds_copy<T>(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
+  int ginf[NT];
+  {
+    const int* gi = (const int*)(p.vblob + o.ginfo);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      const int w = gi[g < V ? g : V - 1];  // unconditional load (see k_cons load_row)
+      ginf[t] = g < V ? w : 0;
+    }
+  }
+  // this lane's constraint ops, packed in registers (tables read from global / L2)
+  const OpTab tab = global_tab(p);
+  unsigned opw[OPS_REG];
+  const int kops = min(OPS_REG, (tab.n_lane + 63) >> 6);
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    const int c = lane + 64 * k;
+    opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
+  }
+  // the wave's ML-space row buffer: immutable features from x_init (written once)
+  double* xrow = (double*)(smem + L.rows_at + wave * o.rb);
+  {
+    const double* xi = (const double*)(sblob + o.xi);
+    for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
+  const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
+  const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
+  const double* s_mlS = (const double*)(smem + L.c_at + (o.mlS - o.c_at));
+  const double* s_mlM = (const double*)(smem + L.c_at + (o.mlM - o.c_at));
+  const double* s_es = (const double*)(smem + L.e_at + (o.es - o.e_at));
+  const double* s_em = (const double*)(smem + L.e_at + (o.em - o.e_at));
+  const double* s_x0 = (const double*)(smem + L.e_at + (o.x0 - o.e_at));
+  const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
+  const bool l2 = p.norm == 2;
+  for (int c0 = 0; c0 < a.n; c0 += 64 * W) {
+    const int span = min(a.n, c0 + 64 * W) - c0 - wave;
+    const int nrw = span > 0 ? (span + W - 1) / W : 0;
+    // lane k: row k's packed parents (own | oth << 16), crossover draws, destination and
+    // mutations (count | overflow << 3 | (last position + 1) << 4)
+    int par_v = 0, cx0_v = 0, cx1_v = 0, orow_v = 0, mut_v = 0;
+    int mpos[MUT_CAP];
+    double mval[MUT_CAP];
+#pragma unroll
+    for (int q = 0; q < MUT_CAP; ++q) {
+      mpos[q] = -1;
+      mval[q] = 0.0;
+    }
+    const bool mine = lane < nrw;
+    const int irow = c0 + wave + W * lane;
+    if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
+    if (a.mode == 1) {
+      const Rng rng(a.seed, a.stream_key);
+      if (mine) {
+        const int nm = a.n / 2;
+        const int m = irow % nm;
+        const int side = irow / nm;
+        const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
+        par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
+        cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
+        cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
+      }
+      const float lq = __log2f(1.0f - 1.0f / (float)V);
+      bool going = mine;
+      int pos = -1, cnt = 0, ovf = 0;
+      double mu[MUT_CAP];
+#pragma unroll 1
+      for (int j = 0; j <= MUT_CAP && __ballot(going); ++j) {
+        bool have = false;
+        double u = 0.0;
+        if (going) {
+          const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+          pos += 1 + geo_gap(s_geo, V, w.x, lq);
+          if (pos >= V) {
+            going = false;
+          } else if (j == MUT_CAP) {
+            ovf = 1;
+            going = false;
+          } else {
+            have = true;
+            u = u53(w.y, w.z);
+            cnt = j + 1;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < MUT_CAP; ++q)
+          if (have && q == j) {
+            mpos[q] = pos;
+            mu[q] = u;
+          }
+      }
+      const double* gl = a.s.gl + (size_t)b * V;
+      const double* gu = a.s.gu + (size_t)b * V;
+      double mlo[MUT_CAP], mhi[MUT_CAP];
+#pragma unroll
+      for (int q = 0; q < MUT_CAP; ++q) {
+        const int mp = mpos[q] < 0 ? 0 : mpos[q];
+        const bool sw = swapped_packed(s_ginfo[mp], cx0_v, cx1_v);
+        mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mp];
+        mlo[q] = gl[mp];
+        mhi[q] = gu[mp];
+      }
+#pragma unroll 1
+      for (int q = 0; q < MUT_CAP && __ballot(q < cnt); ++q) {
+        int gp = 0;
+        double xv = 0.0, u = 0.0, lo = 0.0, hi = 0.0;
+#pragma unroll
+        for (int r = 0; r < MUT_CAP; ++r)
+          if (r == q) {
+            gp = mpos[r];
+            xv = mval[r];
+            u = mu[r];
+            lo = mlo[r];
+            hi = mhi[r];
+          }
+        if (q < cnt) {
+          xv = mutate_gene(xv, lo, hi, (s_ginfo[gp] & 3) == 0, u, a.eta);
+#pragma unroll
+          for (int r = 0; r < MUT_CAP; ++r)
+            if (r == q) mval[r] = xv;
+        }
+      }
+      int last = -1;
+#pragma unroll
+      for (int q = 0; q < MUT_CAP; ++q)
+        if (q < cnt) last = mpos[q];
+      mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
+    } else if (mine) {
+      par_v = irow | (irow << 16);
+    }
+    auto load_row = [&](int k, double* x) {
+      int Vo = V;
+      asm volatile("" : "+s"(Vo));
+      const int pr = rdl(par_v, k);
+      const int cx0 = rdl(cx0_v, k), cx1 = rdl(cx1_v, k);
+      const double* gown = gin + (size_t)(pr & 0xFFFF) * V;
+      const double* goth = gin + (size_t)(pr >> 16) * V;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int g = lane + 64 * t;
+        x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g < Vo ? g : Vo - 1];
+      }
+    };
+    // child genes -> pool, fp32 ML row, f2, constraint program -> f3 (row k of this wave)
+    auto finish_row = [&](int k, const double* x) {
+      int Vo = V, Dmo = Dm, Dm4o = Dm4;
+      asm volatile("" : "+s"(Vo), "+s"(Dmo), "+s"(Dm4o));
+      const int i = c0 + wave + W * k;
+      const int orow = rdl(orow_v, k);
+      if (a.genes_out) {
+        double* gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (lane + 64 * t < Vo) gout[lane + 64 * t] = x[t];
+      }
+      // ML-space row in the wave's buffer (feature_encoder.py:91-124)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (lane + 64 * t < Vo) {
+          if (IDENT)
+            xrow[(ginf[t] >> 17) & 0x7FFF] = x[t];
+          else
+            scatter_gene(p, xrow, ginf[t], x[t]);
+        }
+      }
+      wave_sync();
+      float* xo = a.xml + ((size_t)b * (a.xml_rows ? a.xml_rows : a.n) + i) * Dm4;
+      double acc = 0.0;
+      if (IDENT) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int j = lane + 64 * t;
+          if (j < Dm4o) {
+            float v = 0.f;
+            if (j < Dmo) {
+              const double xf = x[t];
+              v = (float)(xf * s_mlS[j] + s_mlM[j]);
+              const double d = (xf * s_es[j] + s_em[j]) - s_x0[j];
+              acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
+            }
+            xo[j] = v;
+          }
+        }
+      } else {
+        for (int j = lane; j < Dm4; j += 64) {
+          float v = 0.f;
+          if (j < Dm) {
+            const double xf = xrow[s_mutf[j]];
+            v = (float)(xf * s_mlS[j] + s_mlM[j]);
+            const double d = (xf * s_es[j] + s_em[j]) - s_x0[j];
+            acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
+          }
+          xo[j] = v;
+        }
+      }
+      acc = l2 ? wave_sum(acc) : wave_max(acc);
+      double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+      double* hrow =
+          a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
+      const double f3 = constraints_regs<FULL>(tab, opw, kops, xrow, lane, grow,
+                                               (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
+      if (lane == 0) {
+        double f2 = l2 ? sqrt(acc) : acc;
+        if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
+        if (a.F) {
+          a.F[((size_t)b * a.out_rows + orow) * 3 + 1] = f2;
+          a.F[((size_t)b * a.out_rows + orow) * 3 + 2] = f3;
+        }
+        if (hrow) {
+          hrow[1] = f2;
+          hrow[2] = f3;
+        }
+      }
+      wave_sync();  // the next row overwrites xrow
+    };
+    double xn[NT];
+    if (nrw > 0) load_row(0, xn);
+    for (int k = 0; k < nrw; ++k) {
+      double x[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x[t] = xn[t];
+      if (k + 1 < nrw) load_row(k + 1, xn);
+      if (a.mode == 1) {
+        const int nmut = rdl(mut_v, k) & 7;
+#pragma unroll
+        for (int q = 0; q < MUT_CAP; ++q) {
+          if (q < nmut) {
+            const int pos = rdl(mpos[q], k);
+            const double y = rdl_d(mval[q], k);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              if (pos == lane + 64 * t) x[t] = y;
+          }
+        }
+      }
+      finish_row(k, x);
+    }
+    // rare: rows with more than MUT_CAP mutations are redone with every mutation
+    if (a.mode == 1 && __ballot(mut_v & 8)) {
+      const RowsArgs* ap = &a;
+      const uint64_t seed2 = *(volatile const uint64_t*)&ap->seed;
+      const Rng rng2(seed2, a.stream_key);
+      const double* gl = a.s.gl + (size_t)b * V;
+      const double* gu = a.s.gu + (size_t)b * V;
+      const float lq = __log2f(1.0f - 1.0f / (float)V);
+      for (int k = 0; k < nrw; ++k) {
+        if (!(rdl(mut_v, k) & 8)) continue;
+        const int i = c0 + wave + W * k;
+        double x[NT];
+        load_row(k, x);
+        int pos = -1;
+        for (int j = 0;; ++j) {
+          const u32x4 w = rng2.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+          pos += 1 + geo_gap(s_geo, V, w.x, lq);
+          if (pos >= V) break;
+          double xv = 0.0;
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            if (pos == lane + 64 * t) xv = x[t];
+          if ((pos & 63) == lane) {
+            xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              if (pos == lane + 64 * t) x[t] = xv;
+          }
+        }
+        finish_row(k, x);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Classifier phase: k_mlp2's Dense chain over the n xml rows of one state (64-row tiles),
+// with T threads.  Same k order, same final-layer split into four k quarters, so f1 is
+// bit-identical to k_mlp2's.
+__device__ __forceinline__ TileMap tile_map_w(int nct, int wave, int W) {
+  const int cw = nct >= 3 ? 4 : nct;
+  const int groups = W / cw;
+  int nrt = 4 / groups;
+  if (nrt < 1) nrt = 1;
+  const int g = wave / cw;
+  const int rt0 = g * nrt;
+  return TileMap{wave % cw, rt0, rt0 < 4 ? nrt : 0};
+}
+
+template <int CJ, int T>
+__device__ __forceinline__ void mlp_state(const RowsArgs& a, const int b, const int hist_row0,
+                                          unsigned char* smem) {
+  constexpr int W = T / 64;
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int il = lane & 15, ka = lane >> 4;
+  const int nl = p.n_layers;
+  const int K0 = p.Dm4, N0 = p.dims[1];
+  const int hld = mlp2_hmax(p) + 4;
+  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
+  int* rowst = (int*)smem;
+  float* wl = (float*)(smem + 256);
+  float* bl = wl + Klast * nout;
+  float* A0 = (float*)(smem + mlp2_head(p));
+  float* H = A0;
+  for (int q = tid; q < Klast * nout; q += T) wl[q] = p.W[nl - 1][q];
+  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  const int n = a.n;
+  const size_t rbase = (size_t)b * (a.xml_rows ? a.xml_rows : n);  // the state's first xml row
+  const int ntiles = (n + M2_ROWS - 1) / M2_ROWS;
+  const int nkg0 = K0 >> 4;
+  const int nch = (nkg0 + 3) >> 2;
+  constexpr int U = 1024 / T;  // float4 per thread per 64 x 64 chunk
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const int r0 = tile * M2_ROWS;
+    float4 st[U];
+    auto chunk_load = [&](int c) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = tid + T * u;
+        const int row = idx >> 4, q = idx & 15;
+        const int k = c * 64 + 4 * q < K0 ? c * 64 + 4 * q : K0 - 4;
+        const int rr = r0 + row < n ? r0 + row : n - 1;
+        st[u] = *(const float4*)(a.xml + (rbase + rr) * K0 + k);
+      }
+    };
+    auto chunk_store = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = tid + T * u;
+        const int row = idx >> 4, q = idx & 15;
+        *(float4*)(A0 + buf * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = st[u];
+      }
+    };
+    chunk_load(0);
+    __syncthreads();  // the previous tile's (or phase's) readers of the LDS are done
+    if (tid < M2_ROWS) rowst[tid] = r0 + tid < n ? b : -1;
+    chunk_store(0);
+    __syncthreads();
+    floatx4 acc[CJ][4];
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj)
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const TileMap m0 = tile_map_w(N0 >> 4, wave, W);
+    for (int c = 0; c < nch; ++c) {
+      if (c + 1 < nch) chunk_load(c + 1);
+      const int ng = min(4, nkg0 - 4 * c);
+      if (m0.nrt > 0)
+        mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
+                       p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, m0, il, ka);
+      if (c + 1 < nch) chunk_store((c + 1) & 1);
+      __syncthreads();
+    }
+    for (int l = 0; l + 1 < nl; ++l) {
+      const int N = p.dims[l + 1];
+      const TileMap m = tile_map_w(N >> 4, wave, W);
+      if (l > 0) {
+#pragma unroll
+        for (int cj = 0; cj < CJ; ++cj)
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (m.nrt > 0)
+          mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N,
+                         acc, m, il, ka);
+      }
+      float* out = H + (l & 1) * M2_ROWS * hld;
+#pragma unroll
+      for (int cj = 0; cj < CJ; ++cj) {
+        const int ct = m.cb + 4 * cj;
+        if (ct < (N >> 4)) {
+          const int col = ct * 16 + il;
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) {
+            if (rt >= m.nrt) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int row = (m.rt0 + rt) * 16 + ka * 4 + j;
+              const float bv = l == 0 ? a.s.bias1[(size_t)b * N0 + col] : p.bias[l][col];
+              const float v = acc[cj][rt][j] + bv;
+              out[row * hld + col] = v > 0.f ? v : 0.f;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+    float* part = mlp2_part_inplace(p) ? H + ((nl - 1) & 1) * M2_ROWS * hld
+                                       : A0 + mlp2_region_floats(p);
+    if (wave < 4) {
+      const int kq = Klast >> 2;
+      const float* ir = H + ((nl - 2) & 1) * M2_ROWS * hld + lane * hld + wave * kq;
+      const float* wq = wl + wave * kq * nout;
+      float ps[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) ps[c] = 0.f;
+      for (int k = 0; k < kq; k += 4) {
+        const float4 v = *(const float4*)(ir + k);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (c < nout) {
+            ps[c] = fmaf(v.x, wq[k * nout + c], ps[c]);
+            ps[c] = fmaf(v.y, wq[(k + 1) * nout + c], ps[c]);
+            ps[c] = fmaf(v.z, wq[(k + 2) * nout + c], ps[c]);
+            ps[c] = fmaf(v.w, wq[(k + 3) * nout + c], ps[c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c < nout) part[(wave * M2_ROWS + lane) * nout + c] = ps[c];
+    }
+    __syncthreads();
+    if (tid < M2_ROWS && r0 + tid < n) {
+      float prob[8];
+      float mx = -__builtin_inff();
+      for (int c = 0; c < nout; ++c) {
+        const float* q = part + tid * nout + c;
+        prob[c] = (((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) + q[3 * M2_ROWS * nout]) +
+                  bl[c];
+        mx = prob[c] > mx ? prob[c] : mx;
+      }
+      float den = 0.f;
+      for (int c = 0; c < nout; ++c) {
+        prob[c] = expf(prob[c] - mx);
+        den += prob[c];
+      }
+      const double f1 = (double)(prob[a.s.min_class[b]] / den);
+      const int i = r0 + tid;
+      if (a.F) {
+        const int orow = a.out_map ? a.out_map[(size_t)b * n + i] : i;
+        a.F[((size_t)b * a.out_rows + orow) * 3] = f1;
+      }
+      if (a.hist) a.hist[((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// The phases are separate (non-inlined) functions: inlined into one body, the register
+// allocator kept hundreds of argument scalars live across the generation loop and spilled
+// them (SGPRs into VGPRs, VGPRs into scratch), even with the argument pointer laundered per
+// generation (opaque() below).
+// The argument block is addressed through the TU's __constant__ array inside each phase,
+// so its fields are scalar loads (through a generic pointer they became flat loads, each a
+// VMEM round trip on every use).  b / gen / slot are wave-uniform: readfirstlane says so.
+template <bool IDENT, int NT, bool FULL, int T>
+__device__ __noinline__ void rows_phase(int slot, int va, int b, int gen, int h0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  slot = __builtin_amdgcn_readfirstlane(slot);
+  const AttackArgs& A = c_att[slot];
+  rows_state<IDENT, NT, FULL, T>(__builtin_amdgcn_readfirstlane(va) ? A.va : A.ev,
+                                 __builtin_amdgcn_readfirstlane(b),
+                                 __builtin_amdgcn_readfirstlane(gen),
+                                 __builtin_amdgcn_readfirstlane(h0), smem);
+}
+template <int CJ, int T>
+__device__ __noinline__ void mlp_phase(int slot, int va, int b, int h0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  slot = __builtin_amdgcn_readfirstlane(slot);
+  const AttackArgs& A = c_att[slot];
+  mlp_state<CJ, T>(__builtin_amdgcn_readfirstlane(va) ? A.va : A.ev,
+                   __builtin_amdgcn_readfirstlane(b), __builtin_amdgcn_readfirstlane(h0), smem);
+}
+template <int NWMAX, int T>
+__device__ __noinline__ void survive_phase(int slot, int b, int N, int gen, int next) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  slot = __builtin_amdgcn_readfirstlane(slot);
+  const AttackArgs& A = c_att[slot];
+  survive_state<NWMAX, T>(A.sa, __builtin_amdgcn_readfirstlane(b),
+                          __builtin_amdgcn_readfirstlane(N), __builtin_amdgcn_readfirstlane(gen),
+                          __builtin_amdgcn_readfirstlane(gen) + 1,
+                          __builtin_amdgcn_readfirstlane(next) ? A.parents : nullptr, smem);
+}
+
+// T threads per workgroup; two workgroups per CU (min 2 T / 256 waves per SIMD).
+#ifndef MV_SKIP_ROWS
+#define MV_SKIP_ROWS 0
+#endif
+#ifndef MV_SKIP_MLP
+#define MV_SKIP_MLP 0
+#endif
+#ifndef MV_SKIP_SURV
+#define MV_SKIP_SURV 0
+#endif
+typedef const AttackArgs __attribute__((address_space(4)))* CAtt;
+
+// Phase boundary: the phases hand data to each other through global memory (xml rows -> the
+// classifier, F -> survival, tournament parents / slots -> the next variation), written by
+// some waves and read by others.  A workgroup barrier alone does not wait for a wave's
+// outstanding stores, so every wave drains its memory counters first.
+__device__ __forceinline__ void phase_barrier() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+}
+__device__ __forceinline__ CAtt opaque(CAtt p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (CAtt)v;
+}
+
+template <bool IDENT, int NT, bool FULL, int CJ, int NWMAX, int T>
+__global__ __launch_bounds__(T, 2 * T / 256) void k_attack(int slot) {
+  const CAtt A0 = (CAtt)&c_att[slot];
+  const int B = A0->B, P = A0->P, O = A0->O, G = A0->G;
+  long long* const prof = A0->prof;
+  long long t_rows = 0, t_mlp = 0, t_surv = 0, t0 = 0, t1 = 0;
+#define MV_STAMP(acc)                    \
+  if (prof) {                            \
+    t1 = clock64();                      \
+    acc += t1 - t0;                      \
+    t0 = t1;                             \
+  }
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    if (prof) t0 = clock64();
+    const long long tb = t0;
+    // generation 0: pymoo _initialize -- evaluate the initial population, survival with
+    // n_survive == len(pop) (sets ideal/worst/extremes), first tournament
+    if (!MV_SKIP_ROWS) rows_phase<IDENT, NT, FULL, T>(slot, 0, b, 0, 0);
+    phase_barrier();
+    MV_STAMP(t_rows)
+    if (!MV_SKIP_MLP) mlp_phase<CJ, T>(slot, 0, b, 0);
+    phase_barrier();
+    MV_STAMP(t_mlp)
+    if (!MV_SKIP_SURV) survive_phase<NWMAX, T>(slot, b, P, 0, G > 1);
+    phase_barrier();
+    MV_STAMP(t_surv)
+    for (int g = 1; g < G; ++g) {
+      const int h0 = P + (g - 1) * O;
+      if (!MV_SKIP_ROWS) rows_phase<IDENT, NT, FULL, T>(slot, 1, b, g, h0);
+      phase_barrier();
+      MV_STAMP(t_rows)
+      if (!MV_SKIP_MLP) mlp_phase<CJ, T>(slot, 1, b, h0);
+      phase_barrier();
+      MV_STAMP(t_mlp)
+      if (!MV_SKIP_SURV) survive_phase<NWMAX, T>(slot, b, P + O, g, g + 1 < G);
+      phase_barrier();
+      MV_STAMP(t_surv)
+    }
+    if (prof && threadIdx.x == 0) {
+      prof[(size_t)b * 4 + 0] = t_rows;
+      prof[(size_t)b * 4 + 1] = t_mlp;
+      prof[(size_t)b * 4 + 2] = t_surv;
+      prof[(size_t)b * 4 + 3] = t0 - tb;
+    }
+    t_rows = t_mlp = t_surv = 0;
+  }
+#undef MV_STAMP
+}
+
+// Stage `args` in this TU's constant ring (stream-ordered) and launch k_attack<...>: every
+// state resident when it fits (two workgroups per CU), else workgroups loop over states.
+template <bool I, int N, bool F, int C, int NW>
+static hipError_t att_launch(const AttackArgs& args, size_t lds, int grid, hipStream_t stream) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= ATT_MAX_DEV) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lock(g_att_mu);
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)k_attack<I, N, F, C, NW, ATT_T>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+    configured = true;
+  }
+  AttRing& r = g_att[dev];
+  if (!r.ready) {
+    e = hipHostMalloc((void**)&r.host, ATT_SLOTS * sizeof(AttackArgs));
+    for (int i = 0; i < ATT_SLOTS && e == hipSuccess; ++i)
+      e = hipEventCreateWithFlags(&r.ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    r.ready = true;
+  }
+  const int slot = r.next;
+  r.next = (r.next + 1) % ATT_SLOTS;
+  e = hipEventSynchronize(r.ev[slot]);  // the slot's previous launch has finished
+  if (e != hipSuccess) return e;
+  r.host[slot] = args;
+  e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_att), r.host + slot, sizeof(AttackArgs),
+                             (size_t)slot * sizeof(AttackArgs), hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_attack<I, N, F, C, NW, ATT_T>), dim3(grid), dim3(ATT_T), lds, stream,
+                     slot);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipEventRecord(r.ev[slot], stream);
+}
+
+}  // namespace mv

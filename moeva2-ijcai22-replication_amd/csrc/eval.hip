@@ -27,6 +27,7 @@
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
+#include "rowops.h"
 #include "wave.h"
 
 namespace mv {
@@ -76,350 +77,6 @@ hipError_t release_rows(int slot, hipStream_t stream) {
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> lock(g_ring_mu);
   return hipEventRecord(g_rings[dev].ev[slot], stream);
-}
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// numpy float remainder (npy_divmod): result takes the divisor's sign
-__device__ __forceinline__ double py_mod(double a, double b) {
-  double m = fmod(a, b);
-  if (m != 0.0) {
-    if ((b < 0.0) != (m < 0.0)) m += b;
-  } else {
-    m = copysign(0.0, b);
-  }
-  return m;
-}
-
-__device__ __forceinline__ double month_of(double f) {
-  return floor(f / 100.0) * 12.0 + py_mod(f, 100.0);
-}
-
-// Constraint-program tables (ops sorted by code, ABS_SUMDIFF last): global memory
-// (k_constraints) or the LDS copy of the problem blob (k_vary).
-struct OpTab {
-  const int* code;      // [C]
-  const int4* arg;      // [C]
-  const double2* k;     // [C]
-  const int* col;       // [C] original constraint column
-  const int* pool;      // [n_pool]
-  int C, n_lane;        // ops [0, n_lane) lane-parallel, [n_lane, C) ABS_SUMDIFF
-  double tol;
-};
-
-__device__ __forceinline__ OpTab global_tab(const DProblem& p) {
-  OpTab t;
-  t.code = p.op_code;
-  t.arg = (const int4*)p.op_arg;
-  t.k = (const double2*)p.op_k;
-  t.col = p.op_col;
-  t.pool = p.idx_pool;
-  t.C = p.C;
-  t.n_lane = p.C - p.n_sumdiff;
-  t.tol = p.tol;
-  return t;
-}
-
-// One constraint column on the ML row x (LDS).  FULL adds the LCLD financial identities;
-// ABS_SUMDIFF columns are evaluated wave-parallel (sumdiff_wave) by the caller.
-template <bool FULL>
-__device__ __forceinline__ double eval_op(const OpTab& t, int c, const double* __restrict__ x) {
-  const int code = t.code[c];
-  const int4 ar = t.arg[c];
-  switch (code) {
-    case 1:  // MV_OP_DIFF (botnet_constraints.py:283-285)
-      return x[ar.x] - x[ar.y];
-    case 2: {  // MV_OP_RATIO_SAFE (botnet_constraints.py:304-306)
-      const double a = x[ar.x], b = x[ar.y];
-      return (b != 0.0 ? a / b : 0.0) - t.k[c].x;
-    }
-    case 9: {  // MV_OP_XOR_AUG (examples/utils.py:7-29)
-      const double2 k = t.k[c];
-      const bool b1 = x[ar.y] >= k.x;
-      const bool b2 = x[ar.z] >= k.y;
-      return fabs(x[ar.x] - ((b1 != b2) ? 1.0 : 0.0));
-    }
-    default:
-      break;
-  }
-  if (FULL) {
-    switch (code) {
-      case 4: {  // MV_OP_LCLD_INSTALL (lcld_constraints.py:174-177), numpy evaluation order
-        const double x0 = x[ar.x], x1 = x[ar.y], x2 = x[ar.z], x3 = x[ar.w];
-        const double r = x2 / 1200.0;
-        const double base = 1.0 + x2 / 1200.0;
-        const double num = (x0 * r) * pow(base, x1);
-        const double den = pow(base, x1) - 1.0;
-        return fabs(x3 - num / den) - t.k[c].x;
-      }
-      case 5: {  // MV_OP_LCLD_TERM (:186)
-        const double v = x[ar.x];
-        return fabs((36.0 - v) * (60.0 - v));
-      }
-      case 6:  // MV_OP_ABS_RATIO (:189-207)
-        return fabs(x[ar.x] - x[ar.y] / x[ar.z]);
-      case 7:  // MV_OP_MONTHDIFF (:195-201)
-        return fabs(x[ar.x] - (month_of(x[ar.y]) - month_of(x[ar.z])));
-      case 8: {  // MV_OP_RATIO_MASKED (:210-216)
-        const double den = x[ar.z];
-        double ratio = -1.0;
-        if (den != 0.0) {
-          ratio = x[ar.y] / den;
-          if (ratio == __builtin_inf() || ratio != ratio) ratio = -1.0;
-        }
-        return fabs(x[ar.x] - ratio);
-      }
-      default:
-        break;
-    }
-  }
-  return __builtin_nan("");
-}
-
-// |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes, one reduction of the per-lane
-// differences (exact for the integer-valued features of every shipped program; the
-// summation order differs from numpy otherwise).
-__device__ __forceinline__ double sumdiff_wave(const OpTab& t, int c, const double* x, int lane) {
-  const int4 ar = t.arg[c];
-  double s = 0.0;
-  for (int q = ar.x + lane; q < ar.y; q += 64) s += x[t.pool[q]];
-  for (int q = ar.y + lane; q < ar.z; q += 64) s -= x[t.pool[q]];
-  return fabs(wave_sum(s));
-}
-
-// Constraint row -> G columns (+ history columns); returns the wave-uniform f3 = sum(G).
-// Values <= tol -> 0 (Constraints.evaluate); with clamp, G * (G > 0) (default_problem.py:93-97).
-template <bool FULL>
-__device__ __forceinline__ double constraints_row(const OpTab& t, const double* xrow, int lane,
-                                                  double* grow, double* hcols,
-                                                  bool clamp_positive) {
-  double acc3 = 0.0;
-  for (int c = lane; c < t.n_lane; c += 64) {
-    double v = eval_op<FULL>(t, c, xrow);
-    if (v <= t.tol) v = 0.0;
-    const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
-    if (grow) grow[t.col[c]] = g;
-    if (hcols) hcols[t.col[c]] = g;
-    acc3 += g;
-  }
-  for (int c = t.n_lane; c < t.C; ++c) {
-    double v = sumdiff_wave(t, c, xrow, lane);
-    if (v <= t.tol) v = 0.0;
-    const double g = clamp_positive ? v * (v > 0.0 ? 1.0 : 0.0) : v;
-    if (lane == 0) {
-      if (grow) grow[t.col[c]] = g;
-      if (hcols) hcols[t.col[c]] = g;
-      acc3 += g;
-    }
-  }
-  return wave_sum(acc3);
-}
-
-// k_vary's constraint evaluation: each lane keeps its (at most OPS_REG) lane-parallel ops
-// packed in registers -- code (4 bits) | a0 (14) | a1 (14) -- so a row's operand reads are
-// independent LDS loads issued back to back.  DIFF and RATIO_SAFE (the botnet program) are
-// evaluated inline; other codes, and ops beyond OPS_REG per lane, go through eval_op.
-constexpr int OPS_REG = 8;
-
-__device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
-  const int4 ar = t.arg[c];
-  return (unsigned)t.code[c] | ((unsigned)ar.x << 4) | ((unsigned)ar.y << 18);
-}
-
-template <bool FULL>
-__device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigned* opw, int kops,
-                                                   const double* xrow, int lane, double* grow,
-                                                   double* hcols) {
-  double va[OPS_REG], vb[OPS_REG];
-#pragma unroll
-  for (int k = 0; k < OPS_REG; ++k) {
-    if (k < kops) {
-      va[k] = xrow[(opw[k] >> 4) & 0x3FFF];
-      vb[k] = xrow[opw[k] >> 18];
-    }
-  }
-  double acc3 = 0.0;
-#pragma unroll
-  for (int k = 0; k < OPS_REG; ++k) {
-    const int c = lane + 64 * k;
-    if (k < kops && c < t.n_lane) {
-      const int code = opw[k] & 15;
-      double v;
-      if (code == 1)
-        v = va[k] - vb[k];
-      else if (code == 2)
-        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k[c].x;
-      else
-        v = eval_op<FULL>(t, c, xrow);
-      if (v <= t.tol) v = 0.0;
-      const double g = v * (v > 0.0 ? 1.0 : 0.0);
-      if (grow) grow[t.col[c]] = g;
-      if (hcols) hcols[t.col[c]] = g;
-      acc3 += g;
-    }
-  }
-  for (int c = lane + 64 * OPS_REG; c < t.n_lane; c += 64) {
-    double v = eval_op<FULL>(t, c, xrow);
-    if (v <= t.tol) v = 0.0;
-    const double g = v * (v > 0.0 ? 1.0 : 0.0);
-    if (grow) grow[t.col[c]] = g;
-    if (hcols) hcols[t.col[c]] = g;
-    acc3 += g;
-  }
-  double sdsum = 0.0;  // ABS_SUMDIFF columns (wave-uniform values)
-  for (int c = t.n_lane; c < t.C; ++c) {
-    double v = sumdiff_wave(t, c, xrow, lane);
-    if (v <= t.tol) v = 0.0;
-    const double g = v * (v > 0.0 ? 1.0 : 0.0);
-    if (lane == 0) {
-      if (grow) grow[t.col[c]] = g;
-      if (hcols) hcols[t.col[c]] = g;
-    }
-    sdsum += g;
-  }
-  return wave_sum(acc3) + sdsum;
-}
-
-// pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction.
-__device__ __forceinline__ double poly_mut(double x, double xl, double xu, double u, double eta) {
-  const double d1 = (x - xl) / (xu - xl);
-  const double d2 = (xu - x) / (xu - xl);
-  const double mp = 1.0 / (eta + 1.0);
-  double dq;
-  if (u <= 0.5) {
-    const double xy = 1.0 - d1;
-    const double val = 2.0 * u + (1.0 - 2.0 * u) * pow(xy, eta + 1.0);
-    dq = pow(val, mp) - 1.0;
-  } else {
-    const double xy = 1.0 - d2;
-    const double val = 2.0 * (1.0 - u) + 2.0 * (u - 0.5) * pow(xy, eta + 1.0);
-    dq = 1.0 - pow(val, mp);
-  }
-  double y = x + dq * (xu - xl);
-  if (y < xl) y = xl;
-  if (y > xu) y = xu;
-  return y;
-}
-
-// Crossover draws of one mating for one variable-type subset (oracle crossover_draws):
-// on = u53 < prob; genes of the subset with index in [lo, hi) are swapped.
-struct CxSub {
-  int on, lo, hi;
-};
-
-__device__ __forceinline__ CxSub cx_sub(const Rng& rng, int gen, int m, int s, int n,
-                                        double prob) {
-  CxSub c{0, 0, 0};
-  if (n <= 0) return c;
-  const u32x4 w = rng.draw((uint32_t)(m * 2 + s), (uint32_t)gen, TAG_CX);
-  c.on = u53(w.x, w.y) < prob;
-  if (n - 1 <= 0) return c;
-  const int a = 1 + (int)(((uint64_t)w.z * (uint64_t)(n - 1)) >> 32);
-  if (n - 1 == 1) {
-    c.lo = a;
-    c.hi = n;
-  } else {
-    int b = 1 + (int)(((uint64_t)w.w * (uint64_t)(n - 2)) >> 32);
-    if (b >= a) ++b;
-    c.lo = a < b ? a : b;
-    c.hi = a < b ? b : a;
-  }
-  return c;
-}
-
-__device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restrict__ xrow,
-                                             int info, double x) {
-  const int kind = info & 3;
-  const int feat = (info >> 17) & 0x7FFF;
-  if (kind != 2) {
-    xrow[feat] = x;
-  } else {
-    const int o0 = p.ohe_off[feat], o1 = p.ohe_off[feat + 1];
-    for (int k = o0; k < o1; ++k) xrow[p.ohe_feat[k]] = (x == (double)(k - o0)) ? 1.0 : 0.0;
-  }
-}
-
-__device__ __forceinline__ int rdl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
-
-// Geometric gap of the mutation process (oracle mutation_draws): the number of
-// non-mutated genes before the next mutated one is the largest k in [0, V] with
-// w < T[k], T[k] = floor((1 - 1/V)^k * 2^32) (T[0] unused), found by binary search.
-__device__ __forceinline__ int geo_gap(const uint32_t* T, int V, uint32_t w, float lq) {
-  // estimate from log2(w / 2^32) / log2(1 - 1/V), then step to the exact table answer
-  int k = (int)(__log2f(((float)w + 0.5f) * 2.3283064365386963e-10f) / lq);
-  k = k < 0 ? 0 : (k > V ? V : k);
-  while (k < V && w < T[k + 1]) ++k;
-  while (k > 0 && !(w < T[k])) --k;
-  return k;
-}
-
-// MixedVariableMutation of one gene (moeva2.py:104-111): real_pm, or int_pm =
-// IntegerFromFloatMutation (bounds widened by 0.5 - 1e-16, np.round half-to-even, clamp).
-__device__ __forceinline__ double mutate_gene(double x, double xl, double xu, bool is_real,
-                                              double u, double eta) {
-  const double y = poly_mut(x, is_real ? xl : xl - INT_WIDEN, is_real ? xu : xu + INT_WIDEN, u,
-                            eta);
-  if (is_real) return y;
-  double yi = rint(y);
-  if (yi < xl) yi = xl;
-  if (yi > xu) yi = xu;
-  return yi;
-}
-
-__device__ __forceinline__ bool gene_swapped(int info, int on0, int lo0, int hi0, int on1,
-                                             int lo1, int hi1) {
-  const int sub = (info >> 2) & 0x7FFF;
-  return (info & 3) == 0 ? (on0 && sub >= lo0 && sub < hi0) : (on1 && sub >= lo1 && sub < hi1);
-}
-
-constexpr int MUT_CAP = 4;     // mutations per row precomputed in the prologue (registers)
-constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream (V <= 1024)
-
-// Crossover draws of one subset packed into one word: on | lo << 1 | hi << 16.
-__device__ __forceinline__ int pack_cx(const CxSub& c) { return c.on | (c.lo << 1) | (c.hi << 16); }
-__device__ __forceinline__ bool swapped_packed(int info, int cx0, int cx1) {
-  const int sub = (info >> 2) & 0x7FFF;
-  const int c = (info & 3) == 0 ? cx0 : cx1;
-  return (c & 1) && sub >= ((c >> 1) & 0x7FFF) && sub < (c >> 16);
-}
-__device__ __forceinline__ double rdl_d(double v, int k) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
-  return __hiloint2double(hi, lo);
-}
-
-// Async global -> LDS copy of nbytes (a 1-KiB multiple): 16 B per lane, 1 KiB per wave
-// instruction, the workgroup's waves interleaved.
-__device__ __forceinline__ void glds_copy(unsigned char* lds, const unsigned char* g,
-                                          unsigned nbytes, int wave, int lane) {
-  for (unsigned off = wave * 1024u; off < nbytes; off += VARY_T * 16u)
-    __builtin_amdgcn_global_load_lds(g + off + lane * 16, lds + off, 16, 0, 0);
-}
-
-// Rows of one k_gen / k_cons workgroup: a chunk of one state's rows; wave w takes rows
-// i0 + w + 4k (k < nrw).
-struct RowChunk {
-  int b, i0, i1, nrw;
-};
-// XCD-aware order: the dispatcher deals workgroup i to XCD i mod 8, so logical chunk ids
-// are renumbered to keep consecutive ones -- the chunks of one state, which read the same
-// parents and state blob -- on one XCD and its L2.
-__device__ __forceinline__ int xcd_local_id() {
-  constexpr int NX = 8;
-  const int G = gridDim.x, i = blockIdx.x;
-  const int q = G / NX, r = G % NX, x = i % NX, k = i / NX;
-  return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
-}
-__device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
-  RowChunk r;
-  const int nchunk = (n + rows_wg - 1) / rows_wg;
-  const int id = xcd_local_id();
-  r.b = id / nchunk;
-  r.i0 = (id - r.b * nchunk) * rows_wg;
-  r.i1 = min(n, r.i0 + rows_wg);
-  const int span = r.i1 - r.i0 - wave;
-  r.nrw = span > 0 ? (span + 3) / 4 : 0;
-  return r;
 }
 
 // k_gen: variation (mode 1) or gene load (mode 0), the child genes to the pool, the fp32
@@ -1000,96 +657,6 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
 // k_gen through a double-buffered LDS chunk of 64 k (register staged); hidden outputs go to
 // an LDS ping-pong; the immutable features' contribution to layer 0 is the per-state bias
 // bias1 (k_setup_states).  The last Dense + softmax is a dot product per row on the VALU.
-constexpr int M2_ROWS = 64;
-constexpr int M2_ALD = 68;  // layer-0 chunk row stride (floats)
-
-__host__ __device__ inline int mlp2_hmax(const DProblem& p) {
-  int h = 16;
-  for (int l = 1; l < p.n_layers; ++l) h = p.dims[l] > h ? p.dims[l] : h;
-  return h;
-}
-__host__ __device__ inline size_t mlp2_head(const DProblem& p) {
-  const int nl = p.n_layers;
-  return 256 + (((size_t)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~(size_t)15);
-}
-// The hidden ping-pong H aliases the layer-0 chunk buffers (free once layer 0 is done), so
-// four workgroups fit a CU's LDS.
-__host__ __device__ inline int mlp2_region_floats(const DProblem& p) {
-  const int a0 = 2 * M2_ROWS * M2_ALD, h = 2 * M2_ROWS * (mlp2_hmax(p) + 4);
-  return a0 > h ? a0 : h;
-}
-// The final layer's per-wave partial sums [4][M2_ROWS][n_out] go to the free half of the
-// ping-pong when they fit there, else after the region.
-__host__ __device__ inline bool mlp2_part_inplace(const DProblem& p) {
-  return 4 * p.dims[p.n_layers] <= mlp2_hmax(p) + 4;
-}
-__host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
-  return mlp2_head(p) + (size_t)mlp2_region_floats(p) * 4 +
-         (mlp2_part_inplace(p) ? 0 : (size_t)4 * M2_ROWS * p.dims[p.n_layers] * 4);
-}
-
-// A wave's share of a layer's (column tile, row tile) grid: column tiles cb + 4cj over all
-// four row tiles when the layer has >= 3 column tiles, else the waves also split the row
-// tiles (N = 32: two waves per column tile, N = 16: one row tile per wave).
-struct TileMap {
-  int cb, rt0, nrt;
-};
-__device__ __forceinline__ TileMap tile_map(int nct, int wave) {
-  const int cw = nct >= 3 ? 4 : nct;
-  return TileMap{wave % cw, (wave / cw) * cw, cw};
-}
-
-template <int CJ>
-__device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
-                                           const float* __restrict__ Wp, int nkg, int N,
-                                           floatx4 (&acc)[CJ][4], TileMap m, int il, int ka) {
-  const int nct = N >> 4;
-  const int wave = m.cb;
-  // loads are unconditional with clamped indices (a conditional load makes hipcc branch and
-  // wait vmcnt(0), which would drain the next group's prefetch every step)
-  auto load_b = [&](int kg, float4 (&bf)[CJ]) {
-    const int kgc = kg < nkg ? kg : nkg - 1;
-#pragma unroll
-    for (int cj = 0; cj < CJ; ++cj) {
-      const int ct = wave + 4 * cj < nct ? wave + 4 * cj : nct - 1;
-      bf[cj] = *(const float4*)(Wp + ((size_t)kgc * N + ct * 16 + il) * 16 + 4 * ka);
-    }
-  };
-  auto load_a = [&](int kg, float4 (&af)[4]) {
-    const int kgc = kg < nkg ? kg : nkg - 1;
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) {
-      const int r = m.rt0 + (rt < m.nrt ? rt : 0);
-      af[rt] = *(const float4*)(A + (r * 16 + il) * lda + kgc * 16 + 4 * ka);
-    }
-  };
-  float4 bf[CJ], af[4];
-  load_b(0, bf);
-  load_a(0, af);
-  for (int kg = 0; kg < nkg; ++kg) {
-    float4 bn[CJ], an[4];
-    load_b(kg + 1, bn);  // next group's weights (L2) while this group's MFMAs run
-    load_a(kg + 1, an);
-#pragma unroll
-    for (int cj = 0; cj < CJ; ++cj) {
-      if (wave + 4 * cj < nct) {
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          if (rt >= m.nrt) continue;
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].x, bf[cj].x, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].y, bf[cj].y, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].z, bf[cj].z, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].w, bf[cj].w, acc[cj][rt], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
-#pragma unroll
-    for (int rt = 0; rt < 4; ++rt) af[rt] = an[rt];
-  }
-}
-
 template <int CJ>
 __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -112,7 +112,29 @@ __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + (VARY_T / 64) * o.rb;
 }
 
+// fused row phase of the whole-attack kernel: regions B, C, E, then one D-wide row per wave
+struct FusedLds {
+  unsigned b_at, c_at, e_at, rows_at, total;
+};
+__host__ __device__ inline FusedLds fused_lds(const VaryOff& o, int waves) {
+  FusedLds l{};
+  unsigned at = 0;
+  l.b_at = at;
+  at += o.b_end - o.b_at;
+  l.c_at = at;
+  at += o.vb - o.c_at;
+  l.e_at = at;
+  at += o.sb - o.e_at;
+  l.rows_at = at;
+  at += waves * o.rb;
+  l.total = at;
+  return l;
+}
+
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
+size_t attack_lds_bytes(const DProblem& p, int P, int O, int R, int T);
+bool attack_supported(const DProblem& p, int P, int O, int R);
+hipError_t launch_attack(const AttackArgs& args, hipStream_t stream);
 
 // Launch-argument ring (constant memory, per device): stage a copy on `stream`, launch with
 // the returned slot, then release it on the same stream after the slot's last launch.

@@ -47,7 +47,8 @@ __global__ __launch_bounds__(256) void k_objectives(ObjArgs a) {
     vs = vs + a.mm_min[j];
     double v0 = xi[j] * a.mm_scale[j];
     v0 = v0 + a.mm_min[j];
-    bad |= (vs < -1e-4) | (vs > 1.0 + 1e-4) | (v0 < -1e-4) | (v0 > 1.0 + 1e-4);
+    // written as "not inside" so a NaN fails the range like the reference's np.all asserts
+    bad |= !((vs >= -1e-4) & (vs <= 1.0 + 1e-4) & (v0 >= -1e-4) & (v0 <= 1.0 + 1e-4));
     const double d = v0 - vs;
     if (a.norm == 2)
       acc = acc + d * d;
@@ -63,14 +64,15 @@ __global__ __launch_bounds__(256) void k_objectives(ObjArgs a) {
     oh = oh + fabs(1.0 - s);
   }
   oh = wave_sum(oh);
-  // Problem.calc_constraint_violation over [G | ohe]
+  // Problem.calc_constraint_violation over [G | ohe]: sum(G * (G > 0)); a NaN column keeps
+  // the sum NaN (NaN * False = NaN), so such a row never counts as constraint-respecting
   double cv = 0.0;
   const double* __restrict__ gr = a.G + row * a.C;
   for (int c = lane; c < a.C; c += 64) {
     const double v = gr[c];
-    cv = cv + (v > 0.0 ? v : 0.0);
+    cv = cv + (v > 0.0 || v != v ? v : 0.0);
   }
-  cv = wave_sum(cv) + (oh > 0.0 ? oh : 0.0);
+  cv = wave_sum(cv) + (oh > 0.0 || oh != oh ? oh : 0.0);
   const unsigned long long anybad = __ballot(bad);
   if (lane == 0) {
     a.obj[row * 3 + 0] = cv;

@@ -1,0 +1,997 @@
+// R-NSGA-III survival of one initial state's merged population + the next tournament, as
+// a workgroup-level device function (T threads): used by k_survive (one workgroup per
+// state, survive.hip) and by the whole-attack kernel (attack.hip).
+//
+// Restates pymoo 0.4.2.2 (not vendored; [pymoo-recall]):
+//   rnsga3.AspirationPointSurvival._do      ideal/worst, NDS, extreme points, nadir,
+//                                           aspiration ref dirs, association, niching
+//   NonDominatedSorting (fast_non_dominated_sort discovery order, n_stop_if_ranked)
+//   nsga3.get_extreme_points_c / get_nadir_point / associate_to_niches / niching
+//   TournamentSelection(comp_by_cv_then_random) (all CV == 0: random winner)
+// with the dominance relation of src/attacks/moeva2/pareto_operation.py:35-51.
+// Every floating-point expression keeps numpy's evaluation order (the library is built
+// with -ffp-contract=off) so ranks, niches and survivors are bit-identical to
+// oracle/moeva_oracle.py on identical objective arrays.
+//
+// Data: the merged population's F rows (LDS), a dominated-by bitset per individual
+// (ceil(N/64) words), fronts as an ordered index array, niche CSR for the last front.
+#pragma once
+#include <limits.h>
+
+#include "engine.h"
+#include "philox.h"
+#include "wave.h"
+
+namespace mv {
+
+constexpr int SURV_TMAX = 1024;  // largest survival workgroup (reduction scratch sizing)
+
+struct SurvLds {
+  double* F;        // [N*3]
+  double* ref;      // [R*3]
+  double* U;        // [(R+3)*3] normalised reference directions
+  float4* Uf;       // [R+3] the same in fp32 (association pre-filter)
+  double* dist;     // [N]
+  double* red;      // [waves*16] reduction scratch
+  double* scal;     // [40] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9) prev ext(9)
+  unsigned long long* dom;     // [N*NW]
+  unsigned long long* ranked;  // [NW]
+  unsigned long long* cur;     // [NW]
+  int* I;           // [N] fronts concatenated
+  int* pos;         // [N] position in own front
+  int* front_of;    // [N]
+  int* slot;        // [N]
+  int* niche;       // [N]
+  int* memb;        // [N]
+  int* key;         // [N]
+  int* surv;        // [N]
+  int* sel;         // [N]
+  int* fstart;      // [N+2]
+  int* count;       // [R+3]
+  int* remain;      // [R+3]
+  int* csr_off;     // [R+4]
+  int* csr;         // [N]
+  int* cand;        // [R+3]
+  int* ckey;        // [R+3]
+  int* iscal;       // [16]
+  unsigned long long* sortk;  // [max(N, n_perm_slots)] sort keys
+  int* perm;        // [n_perm_slots]
+  unsigned long long* dmin;  // [R+3]
+  int* lround;      // [2N+2] round index of each level
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__host__ __device__ __forceinline__ int pow2_at_least(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// Byte offsets of the survival workspace inside the dynamic LDS block.
+struct SurvOff {
+  unsigned F, ref, U, Uf, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
+      key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm,
+      dmin, lround, total;
+};
+
+__host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
+  const bool dom_lds = N <= SURV_NLDS;
+  const unsigned NW = (N + 63) / 64;
+  const unsigned RN = R + 3;
+  SurvOff o;
+  unsigned off = 0;
+#define TAKE(field, bytes)        \
+  o.field = off;                  \
+  off = (unsigned)align16(off + (size_t)(bytes));
+  TAKE(F, (size_t)N * 3 * 8)
+  TAKE(ref, (size_t)R * 3 * 8)
+  TAKE(U, (size_t)RN * 3 * 8)
+  TAKE(Uf, (size_t)RN * 16)
+  TAKE(dist, (size_t)N * 8)
+  TAKE(red, (SURV_TMAX / 64) * 16 * 8)
+  TAKE(scal, 40 * 8)
+  TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
+  TAKE(ranked, NW * 8)
+  TAKE(cur, NW * 8)
+  TAKE(I, N * 4)
+  TAKE(pos, N * 4)
+  TAKE(front_of, N * 4)
+  TAKE(slot, N * 4)
+  TAKE(niche, N * 4)
+  TAKE(memb, N * 4)
+  TAKE(key, N * 4)
+  TAKE(surv, N * 4)
+  TAKE(sel, N * 4)
+  TAKE(fstart, (N + 2) * 4)
+  TAKE(count, RN * 4)
+  TAKE(remain, RN * 4)
+  TAKE(csr_off, (RN + 1) * 4)
+  TAKE(csr, N * 4)
+  TAKE(cand, RN * 4)
+  TAKE(ckey, RN * 4)
+  TAKE(iscal, 16 * 4)
+  TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
+  TAKE(perm, (size_t)Pperm * 4)
+  TAKE(dmin, (size_t)RN * 8)
+  TAKE(lround, (size_t)(2 * N + 2) * 4)
+#undef TAKE
+  o.total = off;
+  return o;
+}
+
+__device__ __forceinline__ double min_prop(double a, double b) {  // np.min (NaN propagates)
+  double r = b < a ? b : a;
+  r = b != b ? b : r;
+  return a != a ? a : r;
+}
+__device__ __forceinline__ double max_prop(double a, double b) {
+  double r = b > a ? b : a;
+  r = b != b ? b : r;
+  return a != a ? a : r;
+}
+
+// np.argmin order: first NaN, else smallest value, ties -> smallest index
+__device__ __forceinline__ bool arg_better(double v, int i, double bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return (vn && bn) ? (i < bi) : vn;
+  return v < bv || (v == bv && i < bi);
+}
+
+// Ordered stream compaction of the indices i in [0, n) with pred(i) into out[base..].
+// Returns the count (uniform).  Uses red scratch as int[4+1].
+template <int T, class Pred>
+__device__ __forceinline__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int total = 0;
+  for (int b0 = 0; b0 < n; b0 += T) {
+    const int i = b0 + tid;
+    const bool f = i < n && pred(i);
+    const unsigned long long m = __ballot(f);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int woff = 0, all = 0;
+    for (int w = 0; w < T / 64; ++w) {
+      if (w < wave) woff += wsum[w];
+      all += wsum[w];
+    }
+    if (f) out[base + total + woff + before] = i;
+    total += all;
+    __syncthreads();
+  }
+  return total;
+}
+
+// Exclusive prefix sum of v[0, n) in place (LDS); returns the total (uniform).
+template <int T>
+__device__ __forceinline__ int block_scan_excl(int* v, int n, int* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int carry = 0;
+  for (int b0 = 0; b0 < n; b0 += T) {
+    const int i = b0 + tid;
+    const int x = i < n ? v[i] : 0;
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < T / 64; ++w) {
+      const int sw = wsum[w];
+      if (w < wave) woff += sw;
+      tot += sw;
+    }
+    if (i < n) v[i] = carry + woff + incl - x;
+    carry += tot;
+    __syncthreads();
+  }
+  return carry;
+}
+
+__device__ __forceinline__ double wred_min(double v) {
+  return wave_reduce(v, [](double a, double b) { return min_prop(a, b); });
+}
+__device__ __forceinline__ double wred_max(double v) {
+  return wave_reduce(v, [](double a, double b) { return max_prop(a, b); });
+}
+// LAPACK dgetf2/dgetrs-order 3x3 solve (oracle lu_solve3).  Returns false if singular.
+__device__ inline bool lu_solve3(double A[3][3], double x[3]) {
+  for (int k = 0; k < 3; ++k) {
+    int p = k;
+    for (int i = k + 1; i < 3; ++i)
+      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+    if (A[p][k] == 0.0) return false;
+    if (p != k) {
+      for (int j = 0; j < 3; ++j) {
+        const double t = A[k][j];
+        A[k][j] = A[p][j];
+        A[p][j] = t;
+      }
+      const double t = x[k];
+      x[k] = x[p];
+      x[p] = t;
+    }
+    const double r = 1.0 / A[k][k];
+    for (int i = k + 1; i < 3; ++i) A[i][k] = A[i][k] * r;
+    for (int j = k + 1; j < 3; ++j)
+      for (int i = k + 1; i < 3; ++i) A[i][j] = A[i][j] - A[i][k] * A[k][j];
+  }
+  for (int j = 0; j < 3; ++j)
+    for (int i = j + 1; i < 3; ++i) x[i] = x[i] - x[j] * A[i][j];
+  for (int j = 2; j >= 0; --j) {
+    x[j] = x[j] / A[j][j];
+    for (int i = 0; i < j; ++i) x[i] = x[i] - x[j] * A[i][j];
+  }
+  return true;
+}
+
+// Tournament selection for the next generation (oracle tournament_parents).
+template <int T>
+__device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
+                           const int* map_slot, int* out, unsigned long long* sortk,
+                           int* perm) {
+  const int tid = threadIdx.x;
+  const int n_m = (O_next + 1) / 2;
+  const int n_random = n_m * 4;
+  const int n_perms = (n_random + P - 1) / P;
+  const int n = n_perms * P;
+  const Rng rng(seed, sk);
+  int ib = 1;  // bits of the index field
+  while ((1 << ib) < P) ++ib;
+  const unsigned long long imask = (1ull << ib) - 1ull;
+  // permutation q = argsort of its P keys (ties by index): rank of each (key, i) composite
+  // among the P composites of its own permutation
+  for (int idx = tid; idx < n; idx += T) {
+    const int q = idx / P, i = idx - q * P;
+    const unsigned key = rng.draw((uint32_t)idx, (uint32_t)gen, TAG_SEL_PERM).x;
+    sortk[idx] = ((unsigned long long)key << ib) | (unsigned)i;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < n; idx += T) {
+    const int q = idx / P;
+    const unsigned long long kp = sortk[idx];
+    const unsigned long long* kq = sortk + (size_t)q * P;
+    int r = 0;
+    for (int j = 0; j < P; ++j) r += kq[j] < kp ? 1 : 0;
+    perm[q * P + r] = (int)(kp & imask);
+  }
+  __syncthreads();
+  for (int t = tid; t < 2 * n_m; t += T) {
+    const int a = perm[2 * t], b = perm[2 * t + 1];
+    const unsigned bit = rng.draw((uint32_t)t, (uint32_t)gen, TAG_SEL_CHOICE).x & 1u;
+    const int w = bit ? b : a;
+    out[t] = map_slot ? map_slot[w] : w;
+  }
+}
+
+// NWMAX: dominance words per individual held in registers (N <= 64 NWMAX); above
+// SURV_NLDS the bitsets go to the HBM scratch a.dom_g instead of LDS.
+// a: pointers and sizes (slot or dense mode); b: the state; N, gen, sel_gen and
+// parents_out (NULL: no next tournament) vary per generation in the whole-attack kernel.
+template <int NWMAX, int T>
+__device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, const int N,
+                                              const int gen, const int sel_gen,
+                                              int* const parents_out, unsigned char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int R = a.R, RN = R + 3;
+  const int NW = (N + 63) / 64;
+  const int n_m_next = parents_out ? (a.O_next + 1) / 2 : 0;
+  const int pslots = parents_out ? ((n_m_next * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
+  const SurvOff o = surv_offsets(N, R, pslots);
+  SurvLds L;
+  L.F = (double*)(smem + o.F);
+  L.ref = (double*)(smem + o.ref);
+  L.U = (double*)(smem + o.U);
+  L.Uf = (float4*)(smem + o.Uf);
+  L.dist = (double*)(smem + o.dist);
+  L.red = (double*)(smem + o.red);
+  L.scal = (double*)(smem + o.scal);
+  if (NWMAX * 64 > SURV_NLDS)
+    L.dom = a.dom_g + (size_t)b * a.dom_stride;
+  else
+    L.dom = (unsigned long long*)(smem + o.dom);
+  L.ranked = (unsigned long long*)(smem + o.ranked);
+  L.cur = (unsigned long long*)(smem + o.cur);
+  L.I = (int*)(smem + o.I);
+  L.pos = (int*)(smem + o.pos);
+  L.front_of = (int*)(smem + o.front_of);
+  L.slot = (int*)(smem + o.slot);
+  L.niche = (int*)(smem + o.niche);
+  L.memb = (int*)(smem + o.memb);
+  L.key = (int*)(smem + o.key);
+  L.surv = (int*)(smem + o.surv);
+  L.sel = (int*)(smem + o.sel);
+  L.fstart = (int*)(smem + o.fstart);
+  L.count = (int*)(smem + o.count);
+  L.remain = (int*)(smem + o.remain);
+  L.csr_off = (int*)(smem + o.csr_off);
+  L.csr = (int*)(smem + o.csr);
+  L.cand = (int*)(smem + o.cand);
+  L.ckey = (int*)(smem + o.ckey);
+  L.iscal = (int*)(smem + o.iscal);
+  L.sortk = (unsigned long long*)(smem + o.sortk);
+  L.perm = (int*)(smem + o.perm);
+  L.dmin = (unsigned long long*)(smem + o.dmin);
+  L.lround = (int*)(smem + o.lround);
+  double* ideal = L.scal;
+  double* worst = L.scal + 3;
+  double* wpop = L.scal + 6;
+  double* wfront = L.scal + 9;
+  double* nadir = L.scal + 12;
+  double* ext = L.scal + 15;  // 9
+  double* pext = L.scal + 24;  // 9: the carried extremes, staged at entry
+  const int has_ext = a.has_extreme[b] != 0;
+  // carried ideal / worst, loaded at entry so their latency overlaps the F load
+  const double pre_ideal = tid < 3 ? a.ideal[(size_t)b * 3 + tid] : 0.0;
+  const double pre_worst = tid < 3 ? a.worst[(size_t)b * 3 + tid] : 0.0;
+  const bool slot_mode = a.pop_slot != nullptr;
+#define PHASE(k) \
+  if (a.phase && tid == 0) a.phase[(size_t)b * 16 + (k)] = clock64();
+  PHASE(0)
+
+  // ---- load merged F, ref points
+  for (int m = tid; m < N; m += T) {
+    int s = m;
+    const double* src;
+    if (slot_mode) {
+      s = m < a.P ? a.pop_slot[(size_t)b * a.P + m] : a.free_slot[(size_t)b * a.O + (m - a.P)];
+      src = a.F + ((size_t)b * a.S + s) * 3;
+    } else {
+      src = a.F + ((size_t)b * N + m) * 3;
+    }
+    L.F[m * 3 + 0] = src[0];
+    L.F[m * 3 + 1] = src[1];
+    L.F[m * 3 + 2] = src[2];
+    L.slot[m] = s;
+    L.front_of[m] = -1;
+    L.sel[m] = 0;
+  }
+  for (int r = tid; r < R * 3; r += T) L.ref[r] = a.ref[r];
+  if (tid < 9) pext[tid] = a.extreme[(size_t)b * 9 + tid];
+  for (int q = tid; q < NW; q += T) {
+    L.ranked[q] = 0ull;
+    L.cur[q] = 0ull;
+  }
+  __syncthreads();
+  PHASE(1)
+
+  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population
+  {
+    double mn[3], mx[3], wp[3];
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = __builtin_inf();
+      mx[k] = -__builtin_inf();
+      wp[k] = -__builtin_inf();
+    }
+    for (int m = tid; m < N; m += T)
+      for (int k = 0; k < 3; ++k) {
+        const double v = L.F[m * 3 + k];
+        mn[k] = min_prop(mn[k], v);
+        mx[k] = max_prop(mx[k], v);
+        wp[k] = max_prop(wp[k], v);
+      }
+    for (int r = tid; r < R; r += T)
+      for (int k = 0; k < 3; ++k) {
+        const double v = L.ref[r * 3 + k];
+        mn[k] = min_prop(mn[k], v);
+        mx[k] = max_prop(mx[k], v);
+      }
+    for (int k = 0; k < 3; ++k) {
+      mn[k] = wred_min(mn[k]);
+      mx[k] = wred_max(mx[k]);
+      wp[k] = wred_max(wp[k]);
+    }
+    if (lane == 0)
+      for (int k = 0; k < 3; ++k) {
+        L.red[wave * 16 + k] = mn[k];
+        L.red[wave * 16 + 3 + k] = mx[k];
+        L.red[wave * 16 + 6 + k] = wp[k];
+      }
+    __syncthreads();
+    if (tid < 3) {
+      const int k = tid;
+      double vmn = pre_ideal, vmx = pre_worst;
+      double vwp = -__builtin_inf();
+      for (int w = 0; w < T / 64; ++w) {
+        vmn = min_prop(vmn, L.red[w * 16 + k]);
+        vmx = max_prop(vmx, L.red[w * 16 + 3 + k]);
+        vwp = max_prop(vwp, L.red[w * 16 + 6 + k]);
+      }
+      ideal[k] = vmn;
+      worst[k] = vmx;
+      wpop[k] = vwp;
+    }
+  }
+  PHASE(11)
+
+  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the
+  // unordered 64x64 block pairs (qi <= qj) split into two 32-row halves of block qj; lane
+  // l holds row i = 64 qi + l (NaN past N: dominates nothing).  One pass of the six
+  // compares per (i, j) gives both directions: lt && !gt -> i dominates j (ballot = word qi
+  // of dom[j]); gt && !lt -> j dominates i, gathered per lane into the 32-bit half h of word
+  // qj of dom[i] (off-diagonal pairs only; the diagonal block is covered by its ballots).
+  {
+    unsigned* dom32 = (unsigned*)L.dom;
+    const int n_items = NW * (NW + 1);
+    for (int t = wave; t < n_items; t += T / 64) {
+      const int h = t & 1;
+      int qi = 0, rem = t >> 1;
+      while (rem >= NW - qi) {
+        rem -= NW - qi;
+        ++qi;
+      }
+      const int qj = qi + rem;
+      const int i = qi * 64 + lane;
+      const bool ok = i < N;
+      const double fi0 = ok ? L.F[i * 3 + 0] : __builtin_nan("");
+      const double fi1 = ok ? L.F[i * 3 + 1] : __builtin_nan("");
+      const double fi2 = ok ? L.F[i * 3 + 2] : __builtin_nan("");
+      const int j0 = qj * 64 + h * 32;
+      const int jn = min(32, N - j0);
+      // four independent rows per step (the step is latency-bound: LDS broadcast ->
+      // compares -> ballot); lane jj keeps the ballot of row j0 + jj until the item ends
+      unsigned acc = 0u;
+      unsigned long long mine = 0ull;
+      for (int jj = 0; jj < jn; jj += 4) {
+        double g[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = min(j0 + jj + u, N - 1);
+          g[u][0] = L.F[j * 3];
+          g[u][1] = L.F[j * 3 + 1];
+          g[u][2] = L.F[j * 3 + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool valid = jj + u < jn;
+          const bool lt = (fi0 < g[u][0]) | (fi1 < g[u][1]) | (fi2 < g[u][2]);
+          const bool gt = (fi0 > g[u][0]) | (fi1 > g[u][1]) | (fi2 > g[u][2]);
+          const unsigned long long m = __ballot(valid && lt && !gt);
+          if (lane == jj + u) mine = m;
+          acc |= (valid && gt && !lt) ? (1u << ((jj + u) & 31)) : 0u;
+        }
+      }
+      if (lane < jn) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
+      if (qi != qj && ok) dom32[((size_t)i * NW + qj) * 2 + h] = acc;
+    }
+  }
+  __syncthreads();
+  PHASE(2)
+
+  // ---- fast non-dominated sort (discovery order), stop once >= n_survive ranked
+  int* wsum = L.iscal;  // [0..3]
+  int n0 = block_compact<T>(
+      N,
+      [&](int j) {
+        for (int q = 0; q < NW; ++q)
+          if (L.dom[(size_t)j * NW + q]) return false;
+        return true;
+      },
+      L.I, 0, wsum);
+  for (int k = tid; k < n0; k += T) {
+    const int j = L.I[k];
+    L.pos[j] = k;
+    L.front_of[j] = 0;
+    atomicOr(&L.ranked[j >> 6], 1ull << (j & 63));
+    atomicOr(&L.cur[j >> 6], 1ull << (j & 63));
+  }
+  if (tid == 0) {
+    L.fstart[0] = 0;
+    L.fstart[1] = n0;
+  }
+  __syncthreads();
+  int cum = n0, nf = 1;
+  while (cum < a.n_survive && cum < N) {
+    const int nc = block_compact<T>(
+        N,
+        [&](int j) {
+          if ((L.ranked[j >> 6] >> (j & 63)) & 1ull) return false;
+          for (int q = 0; q < NW; ++q)
+            if (L.dom[(size_t)j * NW + q] & ~L.ranked[q]) return false;
+          return true;
+        },
+        L.memb, 0, wsum);
+    if (nc == 0) break;  // unreachable for an acyclic dominance relation
+    for (int k = tid; k < nc; k += T) {
+      const int j = L.memb[k];
+      int mx = -1;
+      for (int q = 0; q < NW; ++q) {
+        unsigned long long bits = L.dom[(size_t)j * NW + q] & L.cur[q];
+        while (bits) {
+          const int i = q * 64 + __ffsll((long long)bits) - 1;
+          bits &= bits - 1ull;
+          mx = L.pos[i] > mx ? L.pos[i] : mx;
+        }
+      }
+      L.key[k] = mx * N + j;
+    }
+    __syncthreads();
+    for (int k = tid; k < nc; k += T) {
+      const int kk = L.key[k];
+      int r = 0;
+      for (int t = 0; t < nc; ++t) r += L.key[t] < kk;
+      L.I[cum + r] = L.memb[k];
+    }
+    for (int q = tid; q < NW; q += T) L.cur[q] = 0ull;
+    __syncthreads();
+    for (int k = tid; k < nc; k += T) {
+      const int j = L.I[cum + k];
+      L.pos[j] = k;
+      L.front_of[j] = nf;
+      atomicOr(&L.ranked[j >> 6], 1ull << (j & 63));
+      atomicOr(&L.cur[j >> 6], 1ull << (j & 63));
+    }
+    cum += nc;
+    ++nf;
+    if (tid == 0) L.fstart[nf] = cum;
+    __syncthreads();
+  }
+  const int n_ranked = cum;
+  PHASE(3)
+
+  // ---- extreme points (ASF over prev extremes + front 0 + ref points), worst of front
+  {
+    const int ne = has_ext ? 3 : 0;
+    const int ncand = ne + n0 + R;
+    double bv[3];
+    int bi[3];
+    double wf[3];
+    for (int k = 0; k < 3; ++k) {
+      bv[k] = __builtin_inf();
+      bi[k] = INT_MAX;
+      wf[k] = -__builtin_inf();
+    }
+    for (int c = tid; c < ncand; c += T) {
+      double row[3];
+      if (c < ne) {
+        for (int k = 0; k < 3; ++k) row[k] = pext[c * 3 + k];
+      } else if (c < ne + n0) {
+        const int m = L.I[c - ne];
+        for (int k = 0; k < 3; ++k) {
+          row[k] = L.F[m * 3 + k];
+          wf[k] = max_prop(wf[k], row[k]);
+        }
+      } else {
+        for (int k = 0; k < 3; ++k) row[k] = L.ref[(c - ne - n0) * 3 + k];
+      }
+      double d[3];
+      for (int k = 0; k < 3; ++k) {
+        d[k] = row[k] - ideal[k];
+        if (d[k] < 1e-3) d[k] = 0.0;
+      }
+      for (int i = 0; i < 3; ++i) {
+        double asf = -__builtin_inf();
+        for (int k = 0; k < 3; ++k) asf = max_prop(asf, d[k] * (i == k ? 1.0 : 1e6));
+        if (arg_better(asf, c, bv[i], bi[i])) {
+          bv[i] = asf;
+          bi[i] = c;
+        }
+      }
+    }
+    for (int i = 0; i < 3; ++i) {
+      wave_argbest(bv[i], bi[i], [](double v, int i1, double w, int i2) {
+        return arg_better(v, i1, w, i2);
+      });
+      wf[i] = wred_max(wf[i]);
+    }
+    __syncthreads();
+    if (lane == 0)
+      for (int i = 0; i < 3; ++i) {
+        L.red[wave * 16 + i] = bv[i];
+        L.red[wave * 16 + 3 + i] = (double)bi[i];
+        L.red[wave * 16 + 6 + i] = wf[i];
+      }
+    __syncthreads();
+    if (tid < 3) {  // one thread per objective: winner of the extreme-point argmin
+      {
+        const int i = tid;
+        double v = L.red[i];
+        int ix = (int)L.red[3 + i];
+        double w = L.red[6 + i];
+        for (int ww = 1; ww < T / 64; ++ww) {
+          const double ov = L.red[ww * 16 + i];
+          const int oi = (int)L.red[ww * 16 + 3 + i];
+          if (arg_better(ov, oi, v, ix)) {
+            v = ov;
+            ix = oi;
+          }
+          w = max_prop(w, L.red[ww * 16 + 6 + i]);
+        }
+        wfront[i] = w;
+        double row[3];
+        if (ix < ne) {
+          for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
+        } else if (ix < ne + n0) {
+          const int m = L.I[ix - ne];
+          for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
+        } else {
+          for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
+        }
+        for (int k = 0; k < 3; ++k) ext[i * 3 + k] = row[k];
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // nadir (get_nadir_point with the call-site argument swap)
+      double M[3][3], plane[3] = {1.0, 1.0, 1.0};
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) M[i][k] = ext[i * 3 + k] - ideal[k];
+      double Mc[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
+      bool ok = lu_solve3(Mc, plane);
+      double nd[3];
+      if (ok) {
+        double icp[3];
+        for (int k = 0; k < 3; ++k) {
+          icp[k] = 1.0 / plane[k];
+          nd[k] = ideal[k] + icp[k];
+        }
+        bool close = true, small = false;
+        for (int i = 0; i < 3; ++i) {
+          const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
+          close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
+          small = small || (icp[i] <= 1e-6);
+        }
+        if (!close || small) {
+          ok = false;
+        } else {
+          for (int k = 0; k < 3; ++k)
+            if (nd[k] > worst[k]) nd[k] = worst[k];
+        }
+      }
+      if (!ok)
+        for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
+      for (int k = 0; k < 3; ++k) {
+        if (nd[k] - ideal[k] <= 1e-6) nd[k] = wfront[k];
+        nadir[k] = nd[k];
+      }
+    }
+    __syncthreads();
+  }
+  PHASE(4)
+
+  // ---- aspiration reference directions (normalised), R points + 3 extreme axes
+  {
+    const double nv = 1.0 / sqrt(3.0);
+    const double asp = a.mu * (1.0 / 3.0);
+    for (int r = tid; r < RN; r += T) {
+      double res[3];
+      if (r < R) {
+        double l[3];
+        for (int k = 0; k < 3; ++k) l[k] = (L.ref[r * 3 + k] - ideal[k]) / (nadir[k] - ideal[k]);
+        const double dot = (l[0] * nv + l[1] * nv) + l[2] * nv;
+        double inter[3];
+        if (fabs(dot) > 1e-6) {
+          const double d = ((1.0 * nv + 0.0 * nv) + 0.0 * nv) / dot;
+          for (int k = 0; k < 3; ++k) inter[k] = 0.0 + l[k] * d;
+        } else {
+          const double q0 = l[0] - 1.0, q1 = l[1] - 0.0, q2 = l[2] - 0.0;
+          const double t = (q0 * nv + q1 * nv) + q2 * nv;
+          for (int k = 0; k < 3; ++k) inter[k] = l[k] - t * nv;
+        }
+        for (int k = 0; k < 3; ++k) res[k] = asp + (inter[k] - asp);
+        if (!(res[0] > 0.0 && res[1] > 0.0 && res[2] > 0.0)) {
+          for (int k = 0; k < 3; ++k)
+            if (res[k] < 0.0) res[k] = 0.0;
+          const double s = (res[0] + res[1]) + res[2];
+          for (int k = 0; k < 3; ++k) res[k] = res[k] / s;
+        }
+      } else {
+        for (int k = 0; k < 3; ++k) res[k] = (k == r - R) ? 1.0 : 0.0;
+      }
+      const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
+      for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
+      L.Uf[r] = make_float4((float)L.U[r * 3], (float)L.U[r * 3 + 1], (float)L.U[r * 3 + 2], 0.f);
+    }
+    if (tid == 0) L.iscal[15] = 0;
+    __syncthreads();
+  }
+  PHASE(5)
+
+  // ---- association of the ranked individuals (I order) to the nearest direction
+  {
+    double den[3];
+    for (int k = 0; k < 3; ++k) {
+      den[k] = nadir[k] - ideal[k];
+      if (den[k] == 0.0) den[k] = 1e-12;
+    }
+    // Two adjacent lanes per individual, each sweeping half of the directions (N = P + O
+    // individuals on 8 waves would otherwise leave 3 waves idle and double up one SIMD);
+    // the halves combine with lane swaps: fp32 minimum (exact), then the fp64 candidate
+    // minimum in np.argmin's order (arg_better is a total order, so the combination equals
+    // the sequential scan).
+    const int jmid = RN / 2;
+    for (int v = tid; v < 2 * n_ranked; v += T) {
+      const int p = v >> 1, hf = v & 1;
+      const int jlo = hf ? jmid : 0, jhi = hf ? RN : jmid;
+      const int m = L.I[p];
+      double Nn[3];
+      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      // fp32 pre-filter of the squared perpendicular distances, as |N|^2 - (N.u)^2 for the
+      // unit directions u (3 FMAs + 1 per direction).  Its error is below 2e-6 |N|^2
+      // (dot product 3.1e-7 |N|, rounding of u to fp32 1.2e-7, |N|^2 1.8e-7, all relative),
+      // so only directions whose fp32 value is within tol = 3e-5 (|N|^2 + best) of the fp32
+      // minimum can hold the fp64 minimum: those few get the exact fp64 distance and
+      // np.argmin's order (first index among equal sqrt'ed distances).  A NaN or overflow
+      // sends the individual to the full exact pass below.
+      const float n0 = (float)Nn[0], n1 = (float)Nn[1], n2 = (float)Nn[2];
+      const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
+      auto d2f = [&](int j) {
+        const float4 u = L.Uf[j];
+        const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
+        return fmaf(-sp, sp, nn);
+      };
+      if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
+          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0 (both lanes)
+        if (!hf) {
+          L.niche[p] = 0;
+          L.dist[p] = 0.0;
+        }
+        continue;
+      }
+      float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;  // 4 independent chains
+      int j = jlo;
+      for (; j + 4 <= jhi; j += 4) {
+        b0 = fminf(b0, d2f(j));
+        b1 = fminf(b1, d2f(j + 1));
+        b2 = fminf(b2, d2f(j + 2));
+        b3 = fminf(b3, d2f(j + 3));
+      }
+      for (; j < jhi; ++j) b0 = fminf(b0, d2f(j));
+      float best = fminf(fminf(b0, b1), fminf(b2, b3));
+      best = fminf(best, __shfl_xor(best, 1, 64));
+      const float lim = best + 3e-5f * (nn + best);
+      if (lim < __builtin_inff()) {  // false on NaN / inf (the same in both lanes)
+        double bd = __builtin_inf();
+        int bj = 0;
+        auto cand = [&](int j) {  // exact fp64 distance, np.argmin order
+          const double* u = &L.U[j * 3];
+          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+          if (arg_better(dd, j, bd, bj)) {
+            bd = dd;
+            bj = j;
+          }
+        };
+        // second sweep only over the chains whose minimum is within lim (usually just the
+        // chain holding the minimum): chain u = jlo + u + 4k, chain 0 also takes the tail.
+        // d2f is the same expression as in the first sweep, so no candidate is missed, and
+        // arg_better is a total order, so the visiting order does not change the result.
+        const int n4 = (jhi - jlo) >> 2;
+        unsigned cm = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) | (b2 <= lim ? 4u : 0u) |
+                      (b3 <= lim ? 8u : 0u);
+        while (cm) {
+          const int u = __builtin_ctz(cm);
+          cm &= cm - 1u;
+          int k = 0;
+          for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
+            const int jc = jlo + 4 * k + u;
+            const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
+            if (d0 <= lim) cand(jc);
+            if (d1 <= lim) cand(jc + 4);
+            if (d2 <= lim) cand(jc + 8);
+            if (d3 <= lim) cand(jc + 12);
+          }
+          for (; k < n4; ++k) {
+            const int jc = jlo + 4 * k + u;
+            if (d2f(jc) <= lim) cand(jc);
+          }
+          if (u == 0)
+            for (int jc = jlo + 4 * n4; jc < jhi; ++jc)
+              if (d2f(jc) <= lim) cand(jc);
+        }
+        const double od = __shfl_xor(bd, 1, 64);
+        const int oj = __shfl_xor(bj, 1, 64);
+        if (arg_better(od, oj, bd, bj)) {
+          bd = od;
+          bj = oj;
+        }
+        if (!hf) {
+          L.niche[p] = bj;
+          L.dist[p] = bd;
+        }
+      } else if (!hf) {
+        L.key[atomicAdd(&L.iscal[15], 1)] = p;
+      }
+    }
+    __syncthreads();
+    PHASE(10)
+    // exact np.argmin over sqrt'ed distances for the flagged individuals
+    const int n_flag = L.iscal[15];
+    if (a.phase && tid == 0) a.phase[(size_t)b * 16 + 12] = n_flag;
+    for (int t = tid; t < n_flag; t += T) {
+      const int p = L.key[t];
+      const int m = L.I[p];
+      double Nn[3];
+      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      double bd = __builtin_inf();
+      int bj = 0;
+      for (int j = 0; j < RN; ++j) {
+        const double* u = &L.U[j * 3];
+        const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+        const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+        const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+        if (arg_better(dd, j, bd, bj)) {
+          bd = dd;
+          bj = j;
+        }
+      }
+      L.niche[p] = bj;
+      L.dist[p] = bd;
+    }
+    __syncthreads();
+  }
+  PHASE(6)
+
+  // ---- survivor selection: fronts until the last + niching on the last front
+  int n_out;
+  if (n_ranked > a.n_survive) {
+    // Niching in closed form.  With member keys fixed per generation, niche n's picks
+    // follow one order (min-dist member first when its until-front count c_n is 0, then
+    // ascending (key, position)); its j-th pick happens at "level" c_n + j, the loop's
+    // rounds visit the non-empty levels in ascending order, and within a round the
+    // niches go in ascending (round key, niche).  So every pick's output position is a
+    // prefix count over levels plus a rank inside its level: no sequential loop.
+    const int fs = L.fstart[nf - 1];
+    const int Lc = n_ranked - fs;
+    const int n_rem = nf == 1 ? a.n_survive : a.n_survive - fs;
+    const int until = nf == 1 ? 0 : fs;
+    const Rng rng(a.seed, a.stream_key);
+    int* grank = L.memb;
+    int* lev = L.csr;
+    int* cnt = L.count;
+    int* mcnt = L.remain;
+    int* start = L.csr_off;
+    int* bestkr = L.cand;
+    const int* nich = L.niche + fs;
+    const double* dst = L.dist + fs;
+    const int nlev = N + Lc + 1;
+    int* fill = L.ckey;  // [RN] fill counters of the niche member lists
+    int* mem = L.key;    // [Lc] last-front members grouped by niche (order inside a niche
+                         // is arbitrary: only counts are taken over it)
+    for (int n = tid; n < RN; n += T) {
+      cnt[n] = 0;
+      mcnt[n] = 0;
+      L.dmin[n] = ~0ull;
+      bestkr[n] = INT_MAX;
+      fill[n] = 0;
+    }
+    for (int l = tid; l < nlev; l += T) L.lround[l] = 0;
+    unsigned long long* sk = L.sortk;
+    for (int p = tid; p < until; p += T) atomicAdd(&cnt[L.niche[p]], 1);
+    // member order inside each niche: ascending (niche, member key, position); grank = rank
+    for (int p = tid; p < Lc; p += T) {
+      const unsigned key = rng.draw((uint32_t)p, (uint32_t)gen, TAG_NICHE_MEMBER).x;
+      atomicAdd(&mcnt[nich[p]], 1);
+      // (niche, member key, position); positions take 10 bits (N <= 1024)
+      sk[p] = ((unsigned long long)nich[p] << 42) | ((unsigned long long)key << 10) | (unsigned)p;
+    }
+    __syncthreads();
+    for (int p = tid; p < Lc; p += T) {
+      const int np_ = nich[p];
+      if (cnt[np_] == 0)
+        atomicMin(&L.dmin[np_], (unsigned long long)__double_as_longlong(dst[p]));
+    }
+    for (int n = tid; n < RN; n += T) start[n] = mcnt[n];
+    __syncthreads();
+    block_scan_excl<T>(start, RN, wsum);
+    for (int p = tid; p < Lc; p += T) {
+      const int np_ = nich[p];
+      mem[start[np_] + atomicAdd(&fill[np_], 1)] = p;
+    }
+    __syncthreads();
+    // grank = rank of sk[p] among all keys = members of smaller niches (start) + rank inside
+    // its own niche, counted over that niche's members only
+    for (int p = tid; p < Lc; p += T) {
+      const int np_ = nich[p];
+      const unsigned long long kp = sk[p];
+      int r = 0, t = start[np_];
+      const int te = t + mcnt[np_];
+      for (; t + 4 <= te; t += 4) {  // crowded niches: four gathers in flight
+        const int m0 = mem[t], m1 = mem[t + 1], m2 = mem[t + 2], m3 = mem[t + 3];
+        r += (sk[m0] < kp ? 1 : 0) + (sk[m1] < kp ? 1 : 0) + (sk[m2] < kp ? 1 : 0) +
+             (sk[m3] < kp ? 1 : 0);
+      }
+      for (; t < te; ++t) r += sk[mem[t]] < kp ? 1 : 0;
+      grank[p] = start[np_] + r;
+      if (cnt[np_] == 0 && (unsigned long long)__double_as_longlong(dst[p]) == L.dmin[np_])
+        atomicMin(&bestkr[np_], r);
+    }
+    __syncthreads();
+    for (int p = tid; p < Lc; p += T) {
+      const int np_ = nich[p];
+      const int kr = grank[p] - start[np_];
+      int j = kr;
+      if (cnt[np_] == 0) j = kr == bestkr[np_] ? 0 : kr + (kr < bestkr[np_] ? 1 : 0);
+      const int l = cnt[np_] + j;
+      lev[p] = l;
+      L.lround[l] = 1;  // level is non-empty
+    }
+    __syncthreads();
+    block_scan_excl<T>(L.lround, nlev, wsum);  // rounds before each level
+    // output order: ascending (level, round key of the niche, niche); a niche picks at most
+    // once per level, so a pick's rank is its position among the remaining slots
+    for (int p = tid; p < Lc; p += T) {
+      const int l = lev[p];
+      const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)gen,
+                                   TAG_NICHE_PERM).x;
+      // (level, round key, niche) is unique per member (a niche picks at most once per
+      // level), so no position field is needed: niche 11 bits, round key 32, level 21
+      sk[p] = ((unsigned long long)l << 43) | ((unsigned long long)kr << 11) |
+              (unsigned long long)nich[p];
+    }
+    __syncthreads();
+    for (int p = tid; p < Lc; p += T) {
+      const unsigned long long kp = sk[p];
+      int r = 0;
+      for (int q = 0; q < Lc; ++q) r += sk[q] < kp ? 1 : 0;
+      if (r < n_rem) L.surv[until + r] = fs + p;
+    }
+    for (int p = tid; p < until; p += T) L.surv[p] = p;
+    n_out = a.n_survive;
+  } else {
+    for (int p = tid; p < n_ranked; p += T) L.surv[p] = p;
+    n_out = n_ranked;
+  }
+  __syncthreads();
+  PHASE(7)
+
+  // ---- outputs
+  for (int k = tid; k < N; k += T) L.memb[k] = 0;  // selected flags by merged index
+  __syncthreads();
+  for (int k = tid; k < n_out; k += T) {
+    const int m = L.I[L.surv[k]];
+    L.memb[m] = 1;
+    L.sel[k] = L.slot[m];  // new population order -> slot (read by the tournament below)
+    if (slot_mode)
+      a.pop_slot_out[(size_t)b * a.n_survive + k] = L.slot[m];
+    else
+      a.survivors[(size_t)b * a.n_survive + k] = m;
+  }
+  if (!slot_mode)
+    for (int k = n_out + tid; k < a.n_survive; k += T)
+      a.survivors[(size_t)b * a.n_survive + k] = -1;
+  if (a.rank)
+    for (int m = tid; m < N; m += T) a.rank[(size_t)b * N + m] = L.front_of[m];
+  if (a.order)
+    for (int p = tid; p < N; p += T) a.order[(size_t)b * N + p] = p < n_ranked ? L.I[p] : -1;
+  if (a.niche)
+    for (int p = tid; p < N; p += T) a.niche[(size_t)b * N + p] = p < n_ranked ? L.niche[p] : -1;
+  if (a.dist)
+    for (int p = tid; p < N; p += T)
+      a.dist[(size_t)b * N + p] = p < n_ranked ? L.dist[p] : 0.0;
+  if (tid == 0) {
+    if (a.n_ranked) a.n_ranked[b] = n_ranked;
+    for (int k = 0; k < 3; ++k) {
+      a.ideal[(size_t)b * 3 + k] = ideal[k];
+      a.worst[(size_t)b * 3 + k] = worst[k];
+      if (a.nadir) a.nadir[(size_t)b * 3 + k] = nadir[k];
+    }
+    for (int k = 0; k < 9; ++k) a.extreme[(size_t)b * 9 + k] = ext[k];
+    a.has_extreme[b] = 1;
+  }
+  __syncthreads();
+  if (slot_mode && N > a.n_survive) {
+    const int nfree = block_compact<T>(N, [&](int m) { return L.memb[m] == 0; }, L.key, 0, wsum);
+    for (int k = tid; k < nfree; k += T)
+      a.free_slot[(size_t)b * a.O + k] = L.slot[L.key[k]];
+  }
+  __syncthreads();
+  PHASE(8)
+  if (parents_out) {
+    tournament<T>(a.n_survive, a.O_next, a.seed, a.stream_key, sel_gen, slot_mode ? L.sel : nullptr,
+               parents_out + (size_t)b * n_m_next * 2, L.sortk, L.perm);
+  }
+  __syncthreads();
+  PHASE(9)
+#undef PHASE
+}
+
+}  // namespace mv

@@ -24,7 +24,8 @@ EXPORTED = [
     "mv_last_error", "mv_device_count", "mv_engine_create", "mv_engine_destroy",
     "mv_set_states", "mv_evaluate", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
-    "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_mlp_create", "mv_mlp_destroy",
+    "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_set_attack_mode",
+    "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
 ]
 
@@ -96,6 +97,8 @@ def lib():
             "mv_set_profiling": [vp, C.c_int32],
             "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
             "mv_get_phase_times": [vp, _f64p, _i32p],
+            "mv_set_attack_mode": [vp, C.c_int32],
+            "mv_get_attack_time": [vp, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
             "mv_objcalc_create": [C.c_int32, C.POINTER(ObjCalcDesc), C.POINTER(vp)],
@@ -139,6 +142,22 @@ def _stream(stream=None):
 def _arr(a, dtype):
     a = np.ascontiguousarray(a, dtype=dtype)
     return a
+
+
+def norm_code(norm) -> int:
+    """2 for the L2 distance, 0 for L-inf; anything else is rejected like the reference
+    DefaultProblem._obj_distance (default_problem.py:80-88 raises NotImplementedError)."""
+    if isinstance(norm, str):
+        norm = norm.strip().lower()
+        if norm in ("2", "l2"):
+            return 2
+        if norm in ("inf", "np.inf", "linf"):
+            return 0
+    elif norm == 2:
+        return 2
+    elif norm == np.inf:
+        return 0
+    raise ValueError(f"norm {norm!r} is not supported (2 or np.inf)")
 
 
 @dataclass
@@ -202,7 +221,7 @@ class Engine:
         pd.n_pool = int(prog.idx_pool.shape[0])
         pd.idx_pool = P(prog.idx_pool if prog.idx_pool.size else np.zeros(1), np.int32, C.c_int32)
         pd.tol = prog.tol
-        pd.norm = 2 if norm in (2, "2") else 0
+        pd.norm = norm_code(norm)
         pd.scale_objectives = int(bool(scale_objectives))
         md = ModelDesc()
         if weights is not None:
@@ -269,6 +288,17 @@ class Engine:
 
     def set_profiling(self, on: bool):
         check(lib().mv_set_profiling(self._h, int(on)))
+
+    def set_attack_mode(self, mode: str):
+        """"auto": the whole-attack kernel when the problem shape has an instance (default);
+        "chain": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per generation)."""
+        check(lib().mv_set_attack_mode(self._h, {"auto": 0, "chain": 1}[mode]))
+
+    def attack_time(self):
+        """(device ms of the last profiled whole-attack launch, whether it ran as one launch)."""
+        ms, whole = C.c_double(), C.c_int32()
+        check(lib().mv_get_attack_time(self._h, C.byref(ms), C.byref(whole)))
+        return ms.value, bool(whole.value)
 
     def kernel_times(self):
         """Summed device ms of k_vary / k_mlp / k_survive over the last profiled attack."""
@@ -368,7 +398,7 @@ class ObjCalc:
         if ml_scale is not None:
             d.ml_scale = P(ml_scale, np.float64, C.c_double)
             d.ml_min = P(ml_min, np.float64, C.c_double)
-        d.norm = 2 if norm in (2, "2") else 0
+        d.norm = norm_code(norm)
         self._h = C.c_void_p()
         check(lib().mv_objcalc_create(device, C.byref(d), C.byref(self._h)))
         self.device = device

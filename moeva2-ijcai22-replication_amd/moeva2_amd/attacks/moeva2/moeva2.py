@@ -95,6 +95,8 @@ class Moeva2:
 
         x = np.ascontiguousarray(x, dtype=np.float64)
         B = x.shape[0]
+        if B == 0:  # the reference's list comprehension over no states
+            return self._empty_device() + (None,) if return_device else []
         eng = get_engine(self._constraints, self._get_classifier(), self._ml_scaler, self.norm,
                          self._scale_objectives, self.device)
         bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
@@ -134,7 +136,16 @@ class Moeva2:
             genes, F, _ = self.generate(xs, mcs, return_device=True)
             return genes, F
 
-        return generate_sharded(attack, x, minimize_class, group)
+        return generate_sharded(attack, x, minimize_class, group, empty=self._empty_device)
+
+    def _empty_device(self):
+        """Zero-state (genes, F) device tensors of this attack's shapes."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        P, V = self.pop_size(), self._encoder.get_genetic_v_length()
+        return (torch.empty((0, P, V), dtype=torch.float64, device=dev),
+                torch.empty((0, P, 3), dtype=torch.float64, device=dev))
 
     def _result(self, b, x0, genes, F, hist, P, O):
         pop = Population(Individual(genes[i], F[i]) for i in range(P))

@@ -54,7 +54,7 @@ class ObjectiveCalculator:
                          np.asarray(self._min_max_scaler.min_, np.float64),
                          None if mls is None else np.asarray(mls.scale_, np.float64),
                          None if mls is None else np.asarray(mls.min_, np.float64),
-                         2 if self.norm in (2, "2") else 0)
+                         self.norm)
             self._dev = (oc, self._constraints._constraint_engine(),
                          Mlp(mlp.weights, mlp.biases))
         return self._dev

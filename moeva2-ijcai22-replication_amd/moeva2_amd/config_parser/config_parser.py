@@ -1,102 +1,118 @@
-"""Experiment configuration (mirror of src/config_parser/config_parser.py).
+"""Experiment configuration for the MoEvA2 driver.
 
-Same command line as the reference drivers: ``-c FILE`` (yaml/json, repeatable), ``-j JSON``
-(inline json), ``-p key1.key2=value``; later sources override earlier ones key by key
-(mergedeep ``Strategy.REPLACE``, restated here since mergedeep is not a dependency).
-The config hash is the md5 of the sorted-key JSON dump (``get_dict_hash``), so output
-file names match the reference's for the same configuration.
+Behaviour contract (src/config_parser/config_parser.py:70-114, pinned by
+tests/test_driver_cpu.py), implemented independently:
+
+* sources: ``-c FILE`` (.yaml/.yml/.json), ``-j JSON`` (inline object) and
+  ``-p a.b.c=value``; each flag may repeat;
+* merge order: every ``-c`` in command-line order, then every ``-j``, then every ``-p``
+  (the reference walks its argparse namespace in flag-definition order); a later source
+  overrides an earlier one leaf by leaf, nested mappings are merged, lists and scalars are
+  replaced (mergedeep ``Strategy.REPLACE``);
+* ``-p`` values: a token that looks like a plain decimal number is typed the way YAML 1.1
+  types it (so ``42`` -> int, ``0.2`` -> float, but ``1e-3`` stays the string "1e-3");
+  anything else is kept as a string;
+* the config hash is the md5 hex digest of ``json.dumps(config, sort_keys=True)``, which
+  names the driver's output files (metrics_*, x_attacks_*, ...).
 """
-import abc
-import argparse
+from __future__ import annotations
+
 import hashlib
 import json
 import os
 import re
+import sys
+from typing import Dict, Iterable, List, Optional, Tuple
 
 import yaml
 
-
-def value_parser(value):
-    """config_parser.py:11-16: numbers through yaml, everything else stays a string."""
-    special_key = "SPECIAL_KEY"
-    if re.match("^[-+]?[0-9]*\\.?[0-9]+(e[-+]?[0-9]+)?$", value) is None:
-        return str(value)
-    return yaml.safe_load(f"{special_key}: {value}")[special_key]
+_NUMBER = re.compile(r"[-+]?[0-9]*\.?[0-9]+(e[-+]?[0-9]+)?")
+_FLAGS = ("-c", "-j", "-p")  # merge order of the three sources
 
 
-def merge_parameters(a, b):
-    """Deep merge of b into a (dicts merged recursively, anything else replaced)."""
-    for k, v in b.items():
-        if isinstance(v, dict) and isinstance(a.get(k), dict):
-            merge_parameters(a[k], v)
+def value_parser(token: str):
+    """Type a ``-p`` value: plain decimal numbers as YAML reads them, else the string."""
+    if not _NUMBER.fullmatch(token):
+        return str(token)
+    return yaml.safe_load(token)
+
+
+def _read_file(path: str) -> dict:
+    ext = os.path.splitext(path)[1].lower()
+    with open(path, "r") as fh:
+        if ext in (".yaml", ".yml"):
+            return yaml.safe_load(fh) or {}
+        if ext == ".json":
+            return json.load(fh)
+    raise ValueError(f"config file {path!r}: expected .yaml, .yml or .json")
+
+
+def _dotted(assignment: str) -> dict:
+    """``a.b=v`` -> {"a": {"b": typed(v)}}."""
+    if "=" not in assignment:
+        raise ValueError(f"-p {assignment!r}: expected key.sub=value")
+    key, raw = assignment.split("=", 1)
+    node = value_parser(raw)
+    for part in reversed(key.split(".")):
+        node = {part: node}
+    return node
+
+
+_LOADERS = {"-c": _read_file, "-j": lambda s: json.loads(s), "-p": _dotted}
+
+
+def merge_parameters(base: dict, update: dict) -> dict:
+    """Merge ``update`` into ``base`` in place: mappings recurse, other values replace."""
+    stack: List[Tuple[dict, dict]] = [(base, update)]
+    while stack:
+        dst, src = stack.pop()
+        for k, v in src.items():
+            if isinstance(v, dict) and isinstance(dst.get(k), dict):
+                stack.append((dst[k], v))
+            else:
+                dst[k] = v
+    return base
+
+
+def _collect(argv: Iterable[str]) -> Dict[str, List[str]]:
+    """Group the values of -c/-j/-p in command-line order (``-c x`` and ``-c=x`` forms)."""
+    got: Dict[str, List[str]] = {f: [] for f in _FLAGS}
+    it = iter(argv)
+    for tok in it:
+        flag, eq, inline = tok.partition("=")
+        if flag in got and eq:
+            got[flag].append(inline)
+        elif tok in got:
+            try:
+                got[tok].append(next(it))
+            except StopIteration:
+                raise SystemExit(f"error: argument {tok}: expected one argument")
+        elif tok in ("-h", "--help"):
+            print("usage: [-c FILE]... [-j JSON]... [-p key1.key2=value]...")
+            raise SystemExit(0)
         else:
-            a[k] = v
-    return a
+            raise SystemExit(f"error: unrecognized arguments: {tok}")
+    return got
 
 
-class Parser(abc.ABC, metaclass=abc.ABCMeta):
-    def do(self, parameter_value: str):
-        return self._do(parameter_value)
-
-    @abc.abstractmethod
-    def _do(self, parameter_value: str) -> dict:
-        raise NotImplementedError
-
-
-class ConfigFileParser(Parser):
-    def __init__(self):
-        self.file_parsers = {".yaml": yaml.safe_load, ".yml": yaml.safe_load, ".json": json.load}
-
-    def _do(self, parameter_value: str) -> dict:
-        extension = os.path.splitext(parameter_value)[1]
-        with open(parameter_value, "r") as f:
-            return self.file_parsers[extension](f)
+def get_config(argv: Optional[Iterable[str]] = None) -> dict:
+    """Merged configuration of a driver command line (default: ``sys.argv[1:]``)."""
+    sources = _collect(sys.argv[1:] if argv is None else argv)
+    config: dict = {}
+    for flag in _FLAGS:
+        for value in sources[flag]:
+            merge_parameters(config, _LOADERS[flag](value))
+    return config
 
 
-class StrParser(Parser):
-    @staticmethod
-    def key_value_to_dict(key, value):
-        splits = key.split(".", maxsplit=1)
-        if len(splits) == 1:
-            return {splits[0]: value}
-        return {splits[0]: StrParser.key_value_to_dict(splits[1], value)}
-
-    def _do(self, parameter_value: str) -> dict:
-        key, value = str(parameter_value).split("=", maxsplit=1)
-        return StrParser.key_value_to_dict(key, value_parser(value))
-
-
-class InlineJsonParser(Parser):
-    def _do(self, parameter_value: str) -> dict:
-        return json.loads(str(parameter_value))
-
-
-def get_config(argv=None):
-    parser = argparse.ArgumentParser()
-    actions = {
-        parser.add_argument("-c", help="Provide config file in yaml or json.",
-                            action="append").dest: ConfigFileParser(),
-        parser.add_argument("-j", help="Inline json.", action="append").dest: InlineJsonParser(),
-        parser.add_argument("-p", help="Provide extra parameters on the form key1.key2=value.",
-                            action="append").dest: StrParser(),
-    }
-    args = vars(parser.parse_args(argv))
-    current = {}
-    for key in args:  # argparse order: -c files, then -j, then -p (as the reference)
-        if args[key] is not None:
-            for value in args[key]:
-                merge_parameters(current, actions[key].do(value))
-    return current
-
-
-def get_dict_hash(dictionary):
+def get_dict_hash(dictionary: dict) -> str:
     return hashlib.md5(json.dumps(dictionary, sort_keys=True).encode("utf-8")).hexdigest()
 
 
-def get_config_hash(config=None, argv=None):
+def get_config_hash(config: Optional[dict] = None, argv=None) -> str:
     return get_dict_hash(get_config(argv) if config is None else config)
 
 
-def save_config(pre_path, config):
-    with open(f"{pre_path}{get_dict_hash(config)}.yaml", "w") as f:
-        yaml.safe_dump(config, f)
+def save_config(pre_path: str, config: dict) -> None:
+    with open(f"{pre_path}{get_dict_hash(config)}.yaml", "w") as fh:
+        yaml.safe_dump(config, fh)

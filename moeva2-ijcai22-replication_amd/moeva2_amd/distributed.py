@@ -10,7 +10,7 @@ the per-state results to every rank.
 from __future__ import annotations
 
 import math
-from typing import Callable, Sequence, Tuple
+from typing import Callable, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -44,9 +44,14 @@ def all_gather_states(local, n_states: int, group=None):
     return torch.cat(parts, dim=0)
 
 
-def generate_sharded(attack: Callable, x: np.ndarray, minimize_class, group=None) -> Sequence:
+def generate_sharded(attack: Callable, x: np.ndarray, minimize_class, group=None,
+                     empty: Optional[Callable] = None) -> Sequence:
     """Run `attack(x_shard, minimize_class_shard) -> tuple of per-state tensors` on this
-    rank's slice of the initial states and all-gather every returned tensor."""
+    rank's slice of the initial states and all-gather every returned tensor.
+
+    A rank whose slice is empty (B < world, or the last ranks when ceil(B/world) leaves a
+    remainder) does not call `attack`: it contributes `empty()` -- zero-row tensors of the
+    shapes `attack` returns -- so every rank still enters the same all_gather."""
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
@@ -54,5 +59,8 @@ def generate_sharded(attack: Callable, x: np.ndarray, minimize_class, group=None
     B = x.shape[0]
     mc = np.broadcast_to(np.asarray(minimize_class), (B,))
     lo, hi = shard_bounds(B, world, rank)
-    outs = attack(x[lo:hi], mc[lo:hi])
+    if hi > lo or empty is None:
+        outs = attack(x[lo:hi], mc[lo:hi])
+    else:
+        outs = empty()
     return tuple(all_gather_states(t, B, group) for t in outs)

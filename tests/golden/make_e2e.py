@@ -1,0 +1,94 @@
+"""End-to-end golden fixtures: the oracle's CPU attack at the benchmark configurations.
+
+TEST INFRASTRUCTURE.  Runs ``oracle.moeva_oracle.run_attack`` (the CPU restatement of
+Moeva2._one_generate + pymoo.minimize, src/attacks/moeva2/moeva2.py:128-171) on every
+initial state of a configuration, one process per host core, and scores each state's final
+population with the oracle ObjectiveCalculator restatement (objective_calculator.py:44-119,
+04_moeva.py:112-131).  The per-state outcome -- which of o1..o7 the final population
+reaches, the best f1, and a digest of the final population -- is committed as
+``tests/golden/e2e_<config>.npz``; ``tests/test_gpu_e2e.py`` runs the device attack at the
+same configuration and compares the success rates (north_star: within 1 pp).
+
+    python tests/golden/make_e2e.py botnet_rq1     # 387 states x 1000 gens (~12 min, 8 cores)
+    python tests/golden/make_e2e.py lcld_rq1_g100   # 64 states x 100 gens
+    python tests/golden/make_e2e.py lcld_rq1_g1000  # 64 states x 1000 gens
+"""
+import hashlib
+import os
+import sys
+import time
+from multiprocessing import get_context
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "moeva2-ijcai22-replication_amd"))
+
+# name: (project, states, n_gen, n_pop, n_off, seed, eps, thr)  -- config/rq1.*.yaml
+CONFIGS = {
+    "botnet_rq1": ("botnet", 387, 1000, 200, 100, 42, 4.0, 0.5),
+    "lcld_rq1_g100": ("lcld", 64, 100, 200, 100, 42, 0.2, 0.25),
+    "lcld_rq1_g1000": ("lcld", 64, 1000, 200, 100, 42, 0.2, 0.25),
+}
+
+_P = None
+
+
+def _init(project):
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from threadpoolctl import threadpool_limits
+
+    threadpool_limits(1)
+    global _P
+    from oracle.problems import Project
+
+    _P = Project(project)
+
+
+def digest(X: np.ndarray) -> int:
+    """First 8 bytes of the sha256 of the final population's genes (float64, C order)."""
+    h = hashlib.sha256(np.ascontiguousarray(X, np.float64).tobytes()).digest()
+    return int.from_bytes(h[:8], "little") & 0x7FFFFFFFFFFFFFFF
+
+
+def one_state(args):
+    b, n_gen, n_pop, n_off, seed, eps, thr = args
+    from oracle import moeva_oracle as mo
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    p = _P
+    ref = energy_ref_dirs(3, n_pop, seed=1)
+    r = mo.run_attack(p.problem(p.x[b], norm=2), ref, n_gen, n_pop + 3, n_off, seed)
+    x_f = mo.genetic_to_ml(p.lay, r.pop_X, p.x[b])
+    sc, mn = p.ml
+    obj = mo.objectives_calc(p.x[b], x_f, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                             1, sc, mn, 2)
+    resp = mo.objectives_respected(obj, thr, eps).any(axis=0)
+    return b, resp, float(obj[:, 1].min()), digest(r.pop_X)
+
+
+def main(name, procs=None):
+    project, B, n_gen, n_pop, n_off, seed, eps, thr = CONFIGS[name]
+    procs = procs or os.cpu_count()
+    t0 = time.time()
+    resp = np.zeros((B, 7), bool)
+    best = np.zeros(B)
+    dig = np.zeros(B, np.int64)
+    jobs = [(b, n_gen, n_pop, n_off, seed, eps, thr) for b in range(B)]
+    with get_context("spawn").Pool(procs, initializer=_init, initargs=(project,)) as pool:
+        for k, (b, r, f1, d) in enumerate(pool.imap_unordered(one_state, jobs)):
+            resp[b], best[b], dig[b] = r, f1, d
+            if (k + 1) % max(1, B // 20) == 0:
+                print(f"{name}: {k + 1}/{B} states, {time.time() - t0:.0f} s", flush=True)
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"e2e_{name}.npz")
+    np.savez_compressed(out, project=project, n_states=B, n_gen=n_gen, n_pop=n_pop,
+                        n_offsprings=n_off, seed=seed, eps=eps, thr=thr, respected=resp,
+                        best_f1=best, pop_digest=dig, success_rate=resp.mean(axis=0),
+                        cpu_seconds=time.time() - t0, procs=procs)
+    print(name, "success rates o1..o7", resp.mean(axis=0), f"{time.time() - t0:.0f} s")
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(CONFIGS):
+        main(n)

@@ -18,11 +18,19 @@ def _free_port():
 
 
 def fake_attack(x, mc):
-    """A deterministic per-state stand-in for Moeva2.generate(return_device=True)."""
+    """A deterministic per-state stand-in for Moeva2.generate(return_device=True); like the
+    engine (mv_set_states rejects B = 0) it refuses an empty slice."""
+    if len(x) == 0:
+        raise ValueError("bad mv_set_states arguments")
     xs = torch.as_tensor(np.asarray(x, np.float64))
     genes = xs[:, None, :].repeat(1, 3, 1) * torch.arange(1, 4, dtype=torch.float64)[None, :, None]
     F = torch.stack([xs.sum(1), xs.max(1).values, torch.as_tensor(mc, dtype=torch.float64)], 1)
     return genes, F[:, None, :]
+
+
+def fake_empty():
+    return (torch.empty((0, 3, 5), dtype=torch.float64),
+            torch.empty((0, 1, 3), dtype=torch.float64))
 
 
 def _worker(rank, world, port, B, q):
@@ -33,14 +41,16 @@ def _worker(rank, world, port, B, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
-    genes, F = generate_sharded(fake_attack, x, np.arange(B) % 2)
+    genes, F = generate_sharded(fake_attack, x, np.arange(B) % 2, empty=fake_empty)
     q.put((rank, genes.numpy(), F.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [7, 8, 1])
-def test_sharded_attack_gathers_every_state(B):
+@pytest.mark.parametrize("B,world", [(7, 2), (8, 2), (1, 2), (5, 4), (2, 3)])
+def test_sharded_attack_gathers_every_state(B, world):
+    """Every rank ends with every state in state order, including ranks whose slice is
+    empty (B < world, or ceil(B/world) leaving the last ranks nothing)."""
     import torch.multiprocessing as mp
 
     from moeva2_amd.distributed import shard_bounds
@@ -48,7 +58,7 @@ def test_sharded_attack_gathers_every_state(B):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, B, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -60,4 +70,6 @@ def test_sharded_attack_gathers_every_state(B):
     for _, genes, F in res:  # every rank holds every state, in state order
         np.testing.assert_array_equal(genes, ref_g.numpy())
         np.testing.assert_array_equal(F, ref_F.numpy())
-    assert [shard_bounds(B, 2, r) for r in range(2)] == [(0, (B + 1) // 2), ((B + 1) // 2, B)]
+    per = -(-B // world)
+    assert [shard_bounds(B, world, r) for r in range(world)] == \
+        [(min(r * per, B), min(r * per + per, B)) for r in range(world)]

@@ -1,6 +1,6 @@
 """Experiment driver / sweep plumbing on CPU (no GPU calls): config parsing and hashing
-(src/config_parser/config_parser.py), path resolution, sweep command lines
-(src/run_rq{1,2,3}.py, MoEvA part)."""
+(src/config_parser/config_parser.py) and path resolution.  The sweep runners
+(src/run_rq*.py) are orchestration and out of scope."""
 import hashlib
 import json
 import os
@@ -30,6 +30,23 @@ def test_config_merge_and_value_parsing():
     assert c["paths"]["model"] == "m.model" and c["paths"]["features"].endswith("features.csv")
 
 
+def test_config_source_order_and_errors(tmp_path):
+    """-c files first, then -j, then -p, whatever the command-line order; leaves replace."""
+    from moeva2_amd.config_parser.config_parser import get_config
+
+    f = tmp_path / "a.json"
+    f.write_text(json.dumps({"x": {"y": 1, "z": [1, 2]}, "n": "file"}))
+    c = get_config(["-p", "n=7", "-j", '{"n": "inline", "x": {"z": [9]}}', "-c", str(f)])
+    assert c == {"x": {"y": 1, "z": [9]}, "n": 7}
+    assert get_config(["-p=x.y=2.5"]) == {"x": {"y": 2.5}}
+    for bad in (["-q", "1"], ["-c"]):
+        try:
+            get_config(bad)
+            raise AssertionError("expected SystemExit")
+        except SystemExit:
+            pass
+
+
 def test_config_hash_is_md5_of_sorted_json():
     from moeva2_amd.config_parser.config_parser import get_config_hash, get_dict_hash
 
@@ -54,21 +71,3 @@ def test_resolve_path_falls_back_to_converted_resources(tmp_path):
         raise AssertionError("expected FileNotFoundError")
     except FileNotFoundError:
         pass
-
-
-def test_sweep_commands_match_reference_layout():
-    from moeva2_amd.config_parser.config_parser import get_config
-    from moeva2_amd.run_rq import build_commands, run
-
-    c = get_config(["-c", f"{CFG}/rq1.lcld.yaml"])
-    cmds = build_commands(c, "rq1")
-    assert len(cmds) == 2  # 1 seed x 1 project x 2 budgets
-    assert cmds[0][2] == "moeva2_amd.experiments.united.04_moeva"
-    assert cmds[0][3:] == ["-c", "./config//moeva.yaml", "-c", "./config//rq1.lcld.static.yaml",
-                           "-p", "seed=42", "-p", "budget=100", "-j", '{"eps_list":[0.2]}']
-    c2 = dict(c, scenari=[{"a": 1}, {"b": 2}], models=["m1", "m2", "m3"])
-    assert len(build_commands(c2, "rq2")) == 4 and len(build_commands(c2, "rq3")) == 6
-    assert build_commands(c2, "rq3")[0][-4:-2] == ["-j", '{"paths":{"model":"m1"}}']
-    seen = []
-    assert run(dict(c, attacks=["moeva", "pgd"]), "rq1", launcher=seen.append) == 2
-    assert seen == cmds

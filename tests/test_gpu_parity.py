@@ -274,12 +274,13 @@ def test_variation_vs_oracle(name):
 
 
 # ------------------------------------------------------------------ whole attack
-def _attack(name, X, n_gen, seed, hist=0, P=23, O=10):
+def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto"):
     from moeva2_amd.problem import get_engine
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
     c, clf, sc = make_constraints(name), make_classifier(name), make_scaler(name)
     eng = get_engine(c, clf, sc, 2)
+    eng.set_attack_mode(mode)
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
     ref = energy_ref_dirs(3, P - 3, seed=1) if P - 3 in (200, 640) else \
@@ -302,6 +303,26 @@ def mo_ref_dirs(n):
     from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
 
     return riesz_energy_dirs(3, n, seed=1, n_iter=200)
+
+
+@pytest.mark.parametrize("name,B,P,O,G,hist", [
+    ("botnet", 9, 203, 100, 6, 1), ("botnet_augmented", 3, 43, 20, 5, 2),
+    ("lcld", 37, 203, 100, 7, 2), ("lcld_augmented", 11, 43, 20, 6, 1),
+    ("lcld", 3, 643, 320, 3, 0)])
+def test_whole_attack_kernel_matches_phase_chain(name, B, P, O, G, hist):
+    """The one-launch attack (k_attack: one workgroup per state runs every generation) is
+    bit-identical to the per-phase chain (k_gen, k_cons, k_mlp2, k_survive per generation):
+    final genes, objectives and the whole history."""
+    X = Project(name).x[:B]
+    e1, g1, F1, h1, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="auto")
+    _, whole = e1.attack_time()
+    assert whole, "the shipped layout must run as one launch"
+    e2, g2, F2, h2, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="chain")
+    assert not e2.attack_time()[1]
+    np.testing.assert_array_equal(g1.cpu().numpy(), g2.cpu().numpy())
+    np.testing.assert_array_equal(F1.cpu().numpy(), F2.cpu().numpy())
+    if hist:
+        np.testing.assert_array_equal(h1.cpu().numpy(), h2.cpu().numpy())
 
 
 def test_attack_invariants_lcld():

@@ -1,0 +1,56 @@
+"""Development check: how many states differ between attack modes / repeated runs."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    import torch
+
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    wname = sys.argv[1] if len(sys.argv) > 1 else "rq1.botnet.static"
+    w = dict(bench.WORKLOADS[wname])
+    eng, c = bench.build_engine(w, 0)
+    X = bench.load_states(w)
+    if len(sys.argv) > 2:
+        X = X[: int(sys.argv[2])]
+    B = X.shape[0]
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    ref = energy_ref_dirs(3, w["n_pop"], seed=1)
+    P, O = w["n_pop"] + 3, w["n_off"]
+    V = eng.prog.V
+
+    def run(mode, G):
+        eng.set_attack_mode(mode)
+        eng.attack_run(G, P, O, 42, ref, 0.05, 0)
+        g = torch.empty((B, P, V), dtype=torch.float64, device="cuda")
+        F = torch.empty((B, P, 3), dtype=torch.float64, device="cuda")
+        eng.attack_population(g, F)
+        torch.cuda.synchronize()
+        return g.cpu().numpy(), F.cpu().numpy()
+
+    for G in (2, 3, 5, 10, 30):
+        a1, a2 = run("auto", G), run("auto", G)
+        c1, c2 = run("chain", G), run("chain", G)
+        d = lambda x, y: int(sum(not (np.array_equal(x[0][b], y[0][b]) and
+                                      np.array_equal(x[1][b], y[1][b])) for b in range(B)))
+        bad = [b for b in range(B) if not np.array_equal(a1[1][b], c1[1][b])][:5]
+        print(f"G={G} states differing: auto-auto {d(a1, a2)} chain-chain {d(c1, c2)} "
+              f"auto-chain {d(a1, c1)} first {bad}", flush=True)
+        if bad:
+            b = bad[0]
+            fa, fc = a1[1][b], c1[1][b]
+            rows = np.where((fa != fc).any(1))[0][:3]
+            for r in rows:
+                print("   state", b, "row", r, "auto", fa[r], "chain", fc[r])
+
+
+if __name__ == "__main__":
+    main()
