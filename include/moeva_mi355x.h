@@ -86,8 +86,9 @@ typedef struct mv_engine mv_engine;
 const char* mv_last_error(void);
 int mv_device_count(int32_t* n);
 
-/* Upload problem constants + classifier weights to `device` (model may be NULL for a
- * constraints-only engine). */
+/* Upload problem constants + classifier weights to `device`.  model may be NULL: a
+ * constraints-only engine, or the engine behind a host classifier plugin (mv_evaluate then
+ * leaves f1 to the caller; mv_attack_run needs a model). */
 int mv_engine_create(int32_t device, const mv_problem_desc* problem, const mv_model_desc* model,
                      mv_engine** out);
 void mv_engine_destroy(mv_engine* e);
@@ -103,6 +104,11 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
  * genes dev [B][n][V] -> F dev [B][n][3] (f1 misclassification, f2 distance, f3 constraint sum);
  * G dev [B][n][C] (constraint values after the tol clamp and G*(G>0)) or NULL. */
 int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double* G, void* stream);
+
+/* FeatureEncoder.genetic_to_ml (feature_encoder.py:129-130) on device, for host-evaluated
+ * plugins (a Constraints subclass without a device program, a non-Dense classifier):
+ * genes dev [B][n][V] -> x dev [B][n][D] with the bound states' x_init. */
+int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* stream);
 
 /* Constraints.evaluate (numpy path: values <= tol set to 0) on ML-space rows:
  * x dev [n][D] -> G dev [n][C].  Works on an engine created without a model. */
@@ -129,6 +135,11 @@ int mv_select_parents(int32_t B, int32_t P, int32_t O, uint64_t seed, int32_t ge
 
 /* MixedVariableCrossover(two-point) + MixedVariableMutation(PM, eta 20), no evaluation:
  * pop dev [B][P][V], parents dev [B][O/2][2] -> off dev [B][O][V]. */
+/* Crossover of mv_variation / mv_attack_run: kind 0 = two-point (moeva2.py:90-101, the
+ * reference's operator; default), 1 = SBX (SimulatedBinaryCrossover, pymoo 0.4.2.2
+ * real_sbx / int_sbx semantics with distribution index eta, prob_per_variable 0.5; the
+ * stale comment at moeva2.py:87 names prob 0.9, eta 30).  prob: mating-level probability. */
+int mv_set_crossover(mv_engine* e, int32_t kind, double eta, double prob);
 int mv_variation(mv_engine* e, int32_t P, int32_t O, uint64_t seed, int32_t gen,
                  const double* pop, const int32_t* parents, double* off, void* stream);
 
@@ -181,11 +192,12 @@ typedef struct mv_attack_params {
 /* Whole attack on device: init population + evaluate + (n_gen-1) x {select, vary+evaluate,
  * survive}, no host round trip.  Asynchronous on `stream`.  Replaces Moeva2.generate's
  * per-state pymoo.minimize calls (moeva2.py:128-171, 194-205) for ALL bound states.
- * For the shipped problem layouts it is ONE launch (k_attack: one workgroup per state runs
- * every generation); other shapes, or attack mode 1, run the per-phase kernel chain
- * (k_gen, k_cons, k_mlp2, k_survive per generation).  Both give identical results. */
+ * Two schedules, identical results: the per-phase kernel chain (k_gen, k_cons, k_mlp2,
+ * k_survive per generation, state groups on up to 4 streams) and, for the shipped problem
+ * layouts, ONE launch (k_attack: one workgroup per state runs every generation). */
 int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
-/* 0: whole-attack kernel when available (default), 1: per-phase kernel chain. */
+/* 0: auto (default; currently the chain), 1: per-phase kernel chain, 2: whole-attack kernel
+ * when the problem layout has an instance (else the chain). */
 int mv_set_attack_mode(mv_engine* e, int32_t mode);
 /* Device ms of the last profiled mv_attack_run's k_attack launch (0 if the chain ran) and
  * whether the last run was the whole-attack kernel. */

@@ -117,7 +117,9 @@ struct mv_engine {
     return err;
   }
   // profiling
-  int attack_mode = 0;      // 0: whole-attack kernel when the shape has an instance, 1: chain
+  int cx_kind = 0;          // 0: two-point (reference), 1: SBX
+  double sbx_eta = 30.0, cx_prob = 0.9;
+  int attack_mode = 0;      // 0: auto, 1: per-phase chain, 2: whole-attack kernel
   bool last_whole = false;  // the last mv_attack_run used the whole-attack kernel
   hipEvent_t ev_att[2] = {};
   bool profiling = false;
@@ -212,6 +214,7 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   if (pd->ml_scale) std::memcpy(mls.data(), pd->ml_scale, D * sizeof(double));
   if (pd->ml_min) std::memcpy(mlm.data(), pd->ml_min, D * sizeof(double));
   const int n_ohe_feats = pd->n_ohe > 0 ? pd->ohe_offsets[pd->n_ohe] : 0;
+  p.n_ohe_feat = n_ohe_feats;
   std::vector<int> ohe_off(pd->n_ohe + 1, 0);
   if (pd->n_ohe > 0) std::memcpy(ohe_off.data(), pd->ohe_offsets, (pd->n_ohe + 1) * sizeof(int));
   hipError_t err = hipSuccess;
@@ -234,6 +237,20 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   K((int**)&p.ohe_off, ohe_off.data(), ohe_off.size());
   K((int**)&p.ohe_feat, pd->ohe_feats, n_ohe_feats);
   K((int**)&p.mut_feat, pd->mut_feats, Dm);
+  {  // feature -> gene map of the decoder (mv_decode): -1 immutable, gene | (category+1) << 16
+    std::vector<int> fdec(D, -1);
+    for (int g = 0; g < V; ++g) {
+      if (pd->gene_kind[g] != MV_GENE_OHE) {
+        if (pd->gene_feat[g] >= 0 && pd->gene_feat[g] < D) fdec[pd->gene_feat[g]] = g;
+      } else {
+        const int q = pd->gene_feat[g];
+        for (int k = pd->ohe_offsets[q]; k < pd->ohe_offsets[q + 1]; ++k)
+          if (pd->ohe_feats[k] >= 0 && pd->ohe_feats[k] < D)
+            fdec[pd->ohe_feats[k]] = g | ((k - pd->ohe_offsets[q] + 1) << 16);
+      }
+    }
+    K((int**)&p.fdec, fdec.data(), D);
+  }
   K((double**)&p.ml_scale, mls.data(), D);
   K((double**)&p.ml_min, mlm.data(), D);
   {
@@ -304,6 +321,8 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     put(vo.pool, pd->idx_pool, (size_t)pd->n_pool * 4);
     put(vo.ginfo, info.data(), (size_t)V4 * 4);
     put(vo.mutf, pd->mut_feats, (size_t)Dm * 4);
+    put(vo.ooff, ohe_off.data(), ohe_off.size() * 4);
+    if (n_ohe_feats > 0) put(vo.ofeat, pd->ohe_feats, (size_t)n_ohe_feats * 4);
     // mutation gap table T[k] = floor((1 - 1/V)^k 2^32), k = 0..V (oracle geometric_table)
     std::vector<uint32_t> geo(V + 1);
     const double q = 1.0 - 1.0 / (double)V;
@@ -381,9 +400,9 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
                   const double* xu, const int32_t* minimize_class, void* stream) {
   if (!e || B <= 0 || !x_init || !xl || !xu || !minimize_class)
     return fail(MV_ERR_ARG, "bad mv_set_states arguments");
-  if (!e->has_model) return fail(MV_ERR_STATE, "engine has no classifier");
   HIPCHK(hipSetDevice(e->device));
-  const int nout = e->p.dims[e->p.n_layers];
+  // a model-less engine (host classifier plugin) evaluates f2 / f3 only: no class check
+  const int nout = e->has_model ? e->p.dims[e->p.n_layers] : INT32_MAX;
   for (int b = 0; b < B; ++b)
     if (minimize_class[b] < 0 || minimize_class[b] >= nout)
       return fail(MV_ERR_ARG, "minimize_class out of range");
@@ -426,7 +445,9 @@ static RowsArgs base_rows(const mv_engine* e) {
   a.p = e->p;
   a.s = e->s;
   a.eta = 20.0;
-  a.cx_prob = 0.9;
+  a.cx_prob = e->cx_prob;
+  a.cx_kind = e->cx_kind;
+  a.sbx_eta = e->sbx_eta;
   a.mut_thr = (uint32_t)(4294967296.0 / (double)e->p.V);
   a.do_eval = 1;
   return a;
@@ -451,6 +472,14 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
   HIPCHK(stage_rows(a, (hipStream_t)stream, &slot));
   HIPCHK(launch_rows(a, slot, 0, 0, (hipStream_t)stream));
   HIPCHK(release_rows(slot, (hipStream_t)stream));
+  return MV_OK;
+}
+
+int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* stream) {
+  if (!e || n < 0 || (n > 0 && (!genes || !x))) return fail(MV_ERR_ARG, "bad mv_decode arguments");
+  if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  HIPCHK(hipSetDevice(e->device));
+  HIPCHK(launch_decode(e->p, e->s, e->B, n, genes, x, (hipStream_t)stream));
   return MV_OK;
 }
 
@@ -558,6 +587,9 @@ static int ensure_events(std::vector<hipEvent_t>& v, size_t n) {
 
 int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   if (!e || !prm) return fail(MV_ERR_ARG, "null argument");
+  if (!e->has_model)
+    return fail(MV_ERR_STATE, "mv_attack_run needs a device classifier (hosted plugins run "
+                              "the generation loop from the host)");
   if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
   const int P = prm->pop_size, O = prm->n_offsprings, G = prm->n_gen, R = prm->n_ref;
   if (P < 2 || O < 2 || (O & 1) || G < 1 || R < 1 || R > SURV_RMAX || P + O > SURV_NMAX ||
@@ -635,9 +667,13 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   HIPCHK(hipGetLastError());
   HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
   HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
+  // attack mode: 2 = whole-attack kernel, 1 = per-phase chain, 0 = auto (the chain: measured
+  // faster on every BASELINE config so far); MV_ATTACK=whole|chain overrides
   const char* env_mode = std::getenv("MV_ATTACK");
-  const bool chain = e->attack_mode == 1 || (env_mode && std::strcmp(env_mode, "chain") == 0);
-  e->last_whole = !chain && attack_supported(e->p, P, O, R);
+  int mode = e->attack_mode;
+  if (env_mode && std::strcmp(env_mode, "whole") == 0) mode = 2;
+  if (env_mode && std::strcmp(env_mode, "chain") == 0) mode = 1;
+  e->last_whole = mode == 2 && attack_supported(e->p, P, O, R);
   if (e->last_whole) {
     // the whole GA loop in one launch: one workgroup per state (attack.hip)
     AttackArgs A{};
@@ -862,9 +898,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       hipStream_t st = gs[q];
       const bool prof = e->profiling && q == 0;
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
-      HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
+      HIPCHK(launch_vary(vq[q], slot_va[q], g, hist_row0, st));  // k_rows (or k_gen + k_cons)
       if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
-      HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
       HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));
@@ -926,8 +961,18 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
   return MV_OK;
 }
 
+int mv_set_crossover(mv_engine* e, int32_t kind, double eta, double prob) {
+  if (!e || kind < 0 || kind > 1 || !(eta >= 0.0) || !(prob >= 0.0 && prob <= 1.0))
+    return fail(MV_ERR_ARG, "crossover: kind 0 (two-point) or 1 (SBX), eta >= 0, 0 <= prob <= 1");
+  e->cx_kind = kind;
+  e->sbx_eta = eta;
+  e->cx_prob = prob;
+  return MV_OK;
+}
+
 int mv_set_attack_mode(mv_engine* e, int32_t mode) {
-  if (!e || mode < 0 || mode > 1) return fail(MV_ERR_ARG, "attack mode must be 0 (auto) or 1 (chain)");
+  if (!e || mode < 0 || mode > 2)
+    return fail(MV_ERR_ARG, "attack mode must be 0 (auto), 1 (chain) or 2 (whole)");
   e->attack_mode = mode;
   return MV_OK;
 }
@@ -1013,7 +1058,7 @@ int mv_mlp_create(int32_t device, const mv_model_desc* md, mv_mlp** out) {
   a.D4 = (md->dims[0] + 3) & ~3;
   int hmax = 16;
   for (int l = 1; l < a.n_layers; ++l) hmax = a.dims[l] > hmax ? a.dims[l] : hmax;
-  if (eval_region1_bytes(a.D4, hmax) + (size_t)EVAL_TR * (hmax + 1) * 4 > 160 * 1024) {
+  if (predict_lds_bytes(a.D4, hmax, a.dims[a.n_layers - 1], a.dims[a.n_layers], 16) > 160 * 1024) {
     delete m;
     return fail(MV_ERR_ARG, "model input too wide for the LDS tile");
   }

@@ -27,6 +27,7 @@
 #include "kernels.h"
 #include "philox.h"
 #include "rowops.h"
+#include "rows_fused.h"
 #include "survival.h"
 #include "wave.h"
 
@@ -46,300 +47,6 @@ constexpr int ATT_MAX_DEV = 64;
 AttRing g_att[ATT_MAX_DEV];
 std::mutex g_att_mu;
 }  // namespace
-
-// ---------------------------------------------------------------------------------------
-// Fused row phase: k_gen + k_cons for the n rows of one state on the workgroup's W waves.
-// Wave w takes rows c0 + w + W k of each chunk of 64 W rows (lane k of the wave holds row
-// k's parents, crossover draws and cached mutations, exactly as k_gen).
-template <bool IDENT, int NT, bool FULL, int T>
-__device__ __forceinline__ void rows_state(const RowsArgs& a, const int b, const int gen,
-                                           const int hist_row0, unsigned char* smem) {
-  constexpr int W = T / 64;
-  const DProblem& p = a.p;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // uniform by construction; readfirstlane lets the non-inlined phase keep them in SGPRs
-  const int V = __builtin_amdgcn_readfirstlane(p.V);
-  const int Dm = __builtin_amdgcn_readfirstlane(p.Dm);
-  const int Dm4 = __builtin_amdgcn_readfirstlane(p.Dm4);
-  const VaryOff o = vary_offsets(p);
-  const FusedLds L = fused_lds(o, W);
-  const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
-  glds_copy<T>(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
-  glds_copy<T>(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
-  glds_copy<T>(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
-  int ginf[NT];
-  {
-    const int* gi = (const int*)(p.vblob + o.ginfo);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int g = lane + 64 * t;
-      const int w = gi[g < V ? g : V - 1];  // unconditional load (see k_cons load_row)
-      ginf[t] = g < V ? w : 0;
-    }
-  }
-  // this lane's constraint ops, packed in registers (tables read from global / L2)
-  const OpTab tab = global_tab(p);
-  unsigned opw[OPS_REG];
-  const int kops = min(OPS_REG, (tab.n_lane + 63) >> 6);
-#pragma unroll
-  for (int k = 0; k < OPS_REG; ++k) {
-    const int c = lane + 64 * k;
-    opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
-  }
-  // the wave's ML-space row buffer: immutable features from x_init (written once)
-  double* xrow = (double*)(smem + L.rows_at + wave * o.rb);
-  {
-    const double* xi = (const double*)(sblob + o.xi);
-    for (int f = lane; f < p.D; f += 64) xrow[f] = xi[f];
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
-  const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
-  const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
-  const double* s_mlS = (const double*)(smem + L.c_at + (o.mlS - o.c_at));
-  const double* s_mlM = (const double*)(smem + L.c_at + (o.mlM - o.c_at));
-  const double* s_es = (const double*)(smem + L.e_at + (o.es - o.e_at));
-  const double* s_em = (const double*)(smem + L.e_at + (o.em - o.e_at));
-  const double* s_x0 = (const double*)(smem + L.e_at + (o.x0 - o.e_at));
-  const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
-  const bool l2 = p.norm == 2;
-  for (int c0 = 0; c0 < a.n; c0 += 64 * W) {
-    const int span = min(a.n, c0 + 64 * W) - c0 - wave;
-    const int nrw = span > 0 ? (span + W - 1) / W : 0;
-    // lane k: row k's packed parents (own | oth << 16), crossover draws, destination and
-    // mutations (count | overflow << 3 | (last position + 1) << 4)
-    int par_v = 0, cx0_v = 0, cx1_v = 0, orow_v = 0, mut_v = 0;
-    int mpos[MUT_CAP];
-    double mval[MUT_CAP];
-#pragma unroll
-    for (int q = 0; q < MUT_CAP; ++q) {
-      mpos[q] = -1;
-      mval[q] = 0.0;
-    }
-    const bool mine = lane < nrw;
-    const int irow = c0 + wave + W * lane;
-    if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
-    if (a.mode == 1) {
-      const Rng rng(a.seed, a.stream_key);
-      if (mine) {
-        const int nm = a.n / 2;
-        const int m = irow % nm;
-        const int side = irow / nm;
-        const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
-        par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
-        cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
-        cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
-      }
-      const float lq = __log2f(1.0f - 1.0f / (float)V);
-      bool going = mine;
-      int pos = -1, cnt = 0, ovf = 0;
-      double mu[MUT_CAP];
-#pragma unroll 1
-      for (int j = 0; j <= MUT_CAP && __ballot(going); ++j) {
-        bool have = false;
-        double u = 0.0;
-        if (going) {
-          const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-          pos += 1 + geo_gap(s_geo, V, w.x, lq);
-          if (pos >= V) {
-            going = false;
-          } else if (j == MUT_CAP) {
-            ovf = 1;
-            going = false;
-          } else {
-            have = true;
-            u = u53(w.y, w.z);
-            cnt = j + 1;
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < MUT_CAP; ++q)
-          if (have && q == j) {
-            mpos[q] = pos;
-            mu[q] = u;
-          }
-      }
-      const double* gl = a.s.gl + (size_t)b * V;
-      const double* gu = a.s.gu + (size_t)b * V;
-      double mlo[MUT_CAP], mhi[MUT_CAP];
-#pragma unroll
-      for (int q = 0; q < MUT_CAP; ++q) {
-        const int mp = mpos[q] < 0 ? 0 : mpos[q];
-        const bool sw = swapped_packed(s_ginfo[mp], cx0_v, cx1_v);
-        mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mp];
-        mlo[q] = gl[mp];
-        mhi[q] = gu[mp];
-      }
-#pragma unroll 1
-      for (int q = 0; q < MUT_CAP && __ballot(q < cnt); ++q) {
-        int gp = 0;
-        double xv = 0.0, u = 0.0, lo = 0.0, hi = 0.0;
-#pragma unroll
-        for (int r = 0; r < MUT_CAP; ++r)
-          if (r == q) {
-            gp = mpos[r];
-            xv = mval[r];
-            u = mu[r];
-            lo = mlo[r];
-            hi = mhi[r];
-          }
-        if (q < cnt) {
-          xv = mutate_gene(xv, lo, hi, (s_ginfo[gp] & 3) == 0, u, a.eta);
-#pragma unroll
-          for (int r = 0; r < MUT_CAP; ++r)
-            if (r == q) mval[r] = xv;
-        }
-      }
-      int last = -1;
-#pragma unroll
-      for (int q = 0; q < MUT_CAP; ++q)
-        if (q < cnt) last = mpos[q];
-      mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
-    } else if (mine) {
-      par_v = irow | (irow << 16);
-    }
-    auto load_row = [&](int k, double* x) {
-      int Vo = V;
-      asm volatile("" : "+s"(Vo));
-      const int pr = rdl(par_v, k);
-      const int cx0 = rdl(cx0_v, k), cx1 = rdl(cx1_v, k);
-      const double* gown = gin + (size_t)(pr & 0xFFFF) * V;
-      const double* goth = gin + (size_t)(pr >> 16) * V;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int g = lane + 64 * t;
-        x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g < Vo ? g : Vo - 1];
-      }
-    };
-    // child genes -> pool, fp32 ML row, f2, constraint program -> f3 (row k of this wave)
-    auto finish_row = [&](int k, const double* x) {
-      int Vo = V, Dmo = Dm, Dm4o = Dm4;
-      asm volatile("" : "+s"(Vo), "+s"(Dmo), "+s"(Dm4o));
-      const int i = c0 + wave + W * k;
-      const int orow = rdl(orow_v, k);
-      if (a.genes_out) {
-        double* gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          if (lane + 64 * t < Vo) gout[lane + 64 * t] = x[t];
-      }
-      // ML-space row in the wave's buffer (feature_encoder.py:91-124)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        if (lane + 64 * t < Vo) {
-          if (IDENT)
-            xrow[(ginf[t] >> 17) & 0x7FFF] = x[t];
-          else
-            scatter_gene(p, xrow, ginf[t], x[t]);
-        }
-      }
-      wave_sync();
-      float* xo = a.xml + ((size_t)b * (a.xml_rows ? a.xml_rows : a.n) + i) * Dm4;
-      double acc = 0.0;
-      if (IDENT) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int j = lane + 64 * t;
-          if (j < Dm4o) {
-            float v = 0.f;
-            if (j < Dmo) {
-              const double xf = x[t];
-              v = (float)(xf * s_mlS[j] + s_mlM[j]);
-              const double d = (xf * s_es[j] + s_em[j]) - s_x0[j];
-              acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
-            }
-            xo[j] = v;
-          }
-        }
-      } else {
-        for (int j = lane; j < Dm4; j += 64) {
-          float v = 0.f;
-          if (j < Dm) {
-            const double xf = xrow[s_mutf[j]];
-            v = (float)(xf * s_mlS[j] + s_mlM[j]);
-            const double d = (xf * s_es[j] + s_em[j]) - s_x0[j];
-            acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
-          }
-          xo[j] = v;
-        }
-      }
-      acc = l2 ? wave_sum(acc) : wave_max(acc);
-      double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-      double* hrow =
-          a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
-      const double f3 = constraints_regs<FULL>(tab, opw, kops, xrow, lane, grow,
-                                               (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
-      if (lane == 0) {
-        double f2 = l2 ? sqrt(acc) : acc;
-        if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-        if (a.F) {
-          a.F[((size_t)b * a.out_rows + orow) * 3 + 1] = f2;
-          a.F[((size_t)b * a.out_rows + orow) * 3 + 2] = f3;
-        }
-        if (hrow) {
-          hrow[1] = f2;
-          hrow[2] = f3;
-        }
-      }
-      wave_sync();  // the next row overwrites xrow
-    };
-    double xn[NT];
-    if (nrw > 0) load_row(0, xn);
-    for (int k = 0; k < nrw; ++k) {
-      double x[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) x[t] = xn[t];
-      if (k + 1 < nrw) load_row(k + 1, xn);
-      if (a.mode == 1) {
-        const int nmut = rdl(mut_v, k) & 7;
-#pragma unroll
-        for (int q = 0; q < MUT_CAP; ++q) {
-          if (q < nmut) {
-            const int pos = rdl(mpos[q], k);
-            const double y = rdl_d(mval[q], k);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              if (pos == lane + 64 * t) x[t] = y;
-          }
-        }
-      }
-      finish_row(k, x);
-    }
-    // rare: rows with more than MUT_CAP mutations are redone with every mutation
-    if (a.mode == 1 && __ballot(mut_v & 8)) {
-      const RowsArgs* ap = &a;
-      const uint64_t seed2 = *(volatile const uint64_t*)&ap->seed;
-      const Rng rng2(seed2, a.stream_key);
-      const double* gl = a.s.gl + (size_t)b * V;
-      const double* gu = a.s.gu + (size_t)b * V;
-      const float lq = __log2f(1.0f - 1.0f / (float)V);
-      for (int k = 0; k < nrw; ++k) {
-        if (!(rdl(mut_v, k) & 8)) continue;
-        const int i = c0 + wave + W * k;
-        double x[NT];
-        load_row(k, x);
-        int pos = -1;
-        for (int j = 0;; ++j) {
-          const u32x4 w = rng2.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-          pos += 1 + geo_gap(s_geo, V, w.x, lq);
-          if (pos >= V) break;
-          double xv = 0.0;
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            if (pos == lane + 64 * t) xv = x[t];
-          if ((pos & 63) == lane) {
-            xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              if (pos == lane + 64 * t) x[t] = xv;
-          }
-        }
-        finish_row(k, x);
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------
 // Classifier phase: k_mlp2's Dense chain over the n xml rows of one state (64-row tiles),
@@ -480,20 +187,15 @@ __device__ __forceinline__ void mlp_state(const RowsArgs& a, const int b, const 
     }
     __syncthreads();
     if (tid < M2_ROWS && r0 + tid < n) {
-      float prob[8];
-      float mx = -__builtin_inff();
+      double z[8];
+      double mx = -__builtin_inf();
       for (int c = 0; c < nout; ++c) {
         const float* q = part + tid * nout + c;
-        prob[c] = (((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) + q[3 * M2_ROWS * nout]) +
-                  bl[c];
-        mx = prob[c] > mx ? prob[c] : mx;
+        z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
+                         q[3 * M2_ROWS * nout]) + bl[c]);
+        mx = z[c] > mx ? z[c] : mx;
       }
-      float den = 0.f;
-      for (int c = 0; c < nout; ++c) {
-        prob[c] = expf(prob[c] - mx);
-        den += prob[c];
-      }
-      const double f1 = (double)(prob[a.s.min_class[b]] / den);
+      const double f1 = softmax_pick(z, nout, mx, a.s.min_class[b]);
       const int i = r0 + tid;
       if (a.F) {
         const int orow = a.out_map ? a.out_map[(size_t)b * n + i] : i;
@@ -517,10 +219,10 @@ __device__ __noinline__ void rows_phase(int slot, int va, int b, int gen, int h0
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   slot = __builtin_amdgcn_readfirstlane(slot);
   const AttackArgs& A = c_att[slot];
-  rows_state<IDENT, NT, FULL, T>(__builtin_amdgcn_readfirstlane(va) ? A.va : A.ev,
-                                 __builtin_amdgcn_readfirstlane(b),
+  const RowsArgs& a = __builtin_amdgcn_readfirstlane(va) ? A.va : A.ev;
+  rows_state<IDENT, NT, FULL, T>(a, __builtin_amdgcn_readfirstlane(b),
                                  __builtin_amdgcn_readfirstlane(gen),
-                                 __builtin_amdgcn_readfirstlane(h0), smem);
+                                 __builtin_amdgcn_readfirstlane(h0), 0, a.n, smem);
 }
 template <int CJ, int T>
 __device__ __noinline__ void mlp_phase(int slot, int va, int b, int h0) {

@@ -31,6 +31,7 @@ constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound 
 
 struct DProblem {
   int D, V, Dm, Dm4, C, n_ohe;  // Dm4: mutable features padded to a multiple of 16
+  int n_ohe_feat;         // features of all one-hot groups (ohe_feat length)
   int n_sub[2];           // crossover subsets: 0 real, 1 int (OHE genes are int)
   const int* gene_kind;   // [V]
   const int* gene_feat;   // [V]
@@ -39,6 +40,7 @@ struct DProblem {
   const int* ohe_off;     // [n_ohe+1]
   const int* ohe_feat;
   const int* mut_feat;    // [Dm]
+  const int* fdec;        // [D] decoder: -1 immutable, else gene | (one-hot category + 1) << 16
   const double* ml_scale; // [D]
   const double* ml_min;   // [D]
   const double* mlS;      // [Dm4] ml_scale gathered at the mutable features
@@ -104,6 +106,8 @@ struct RowsArgs {
   uint32_t mut_thr;         // floor(2^32 / V)
   double eta;               // 20
   double cx_prob;           // 0.9
+  int cx_kind;              // 0: two-point (the reference), 1: SBX (north_star option)
+  double sbx_eta;           // SBX distribution index (30)
   int do_eval;              // 0: variation only
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
   int xml_rows;             // whole-attack kernel: xml rows per state (0: n)

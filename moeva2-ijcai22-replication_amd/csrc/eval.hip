@@ -28,6 +28,7 @@
 #include "kernels.h"
 #include "philox.h"
 #include "rowops.h"
+#include "rows_fused.h"
 #include "wave.h"
 
 namespace mv {
@@ -161,12 +162,15 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
     mval[q] = 0.0;
   }
   const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
+  const Rng rng(a.seed, a.stream_key);
+  const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
+  const double* sgu = a.s.gu + (size_t)b * V;
+  const bool sbx = a.mode == 1 && a.cx_kind == 1;
   const bool mine = lane < nrw;
   const int irow = rc.i0 + wave + 4 * lane;
   if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
   if (a.mode == 1) {
-    const Rng rng(a.seed, a.stream_key);
-    if (mine) {
+        if (mine) {
       const int nm = a.n / 2;
       const int m = irow % nm;
       const int side = irow / nm;
@@ -174,10 +178,14 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
       par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
       cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
       cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
+      if (sbx) {  // SBX: the subsets' mating-level draws only (no segment)
+        cx0_v &= 1;
+        cx1_v &= 1;
+      }
     }
     // (1) mutation positions and their PM uniforms
     const float lq = __log2f(1.0f - 1.0f / (float)V);
-    bool going = mine;
+    bool going = mine && !sbx;
     int pos = -1, cnt = 0, ovf = 0;
     double mu[MUT_CAP];
 #pragma unroll 1
@@ -325,7 +333,14 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
 #pragma unroll
     for (int t = 0; t < NT; ++t) x[t] = xn[t];
     if (k + 1 < nrw) load_row(k + 1, xn);
-    if (a.mode == 1) {  // apply the row's cached mutations
+    if (sbx) {  // SBX children, then every mutation of the row
+      const int i = rc.i0 + wave + 4 * k;
+      const int nm = a.n / 2;
+      const int pr = rdl(par_v, k);
+      sbx_row<NT>(x, ginf, gin + (size_t)(pr >> 16) * V, sgl, sgu, V, i % nm, i / nm,
+                  rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen, a.sbx_eta, lane);
+      mutate_row_full<NT>(x, s_geo, s_ginfo, sgl, sgu, V, i, rng, gen, a.eta, lane);
+    } else if (a.mode == 1) {  // apply the row's cached mutations
       const int nmut = rdl(mut_v, k) & 7;
 #pragma unroll
       for (int q = 0; q < MUT_CAP; ++q) {
@@ -475,36 +490,52 @@ __global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_
   }
 }
 
+// k_rows: k_gen + k_cons fused (rows_fused.h): one workgroup = one state x a chunk of its
+// rows; each child row is read (parents) and written once, its constraints evaluated from
+// the wave's LDS row right after the variation -- no re-read of the child genes.
+template <bool IDENT, int NT, bool FULL>
+__global__ __launch_bounds__(VARY_T) void k_rows(int slot, int gen, int hist_row0, int rows_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const int nchunk = (a.n + rows_wg - 1) / rows_wg;
+  const int id = xcd_local_id();
+  const int b = id / nchunk;
+  const int r0 = (id - b * nchunk) * rows_wg;
+  rows_state<IDENT, NT, FULL, VARY_T>(a, b, gen, hist_row0, r0, min(a.n, r0 + rows_wg), smem);
+}
+
 // ---------------------------------------------------------------------------------------
-// Dense layer on MFMA: out[32][N] = relu(in[32][K] . W[K][N] + bias), K % 4 == 0, N % 16 == 0.
-// Software-pipelined: U k-steps of A (LDS) and B (global/L2) fragments are loaded before
-// their 2*U MFMAs so the B-load latency is paid once per U steps.
-template <int MAXCT>
+// Dense layer on MFMA: out[16 RT][N] = relu(in[16 RT][K] . W[K][N] + bias), K % 4 == 0,
+// N % 16 == 0 (RT = 2: the 32-row tiles of k_mlp / k_predict; RT = 1: k_predict's 16-row
+// tiles for inputs too wide for a 32-row LDS tile).  Software-pipelined: U k-steps of A
+// (LDS) and B (global/L2) fragments are loaded before their RT*U MFMAs so the B-load
+// latency is paid once per U steps.
+template <int MAXCT, int RT = 2>
 __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi, int K,
                            const float* __restrict__ W, int N, const float* __restrict__ bias,
                            const float* __restrict__ bias_state, const int* row_state,
                            float* __restrict__ out, int ldo, int wave, int lane) {
   constexpr int U = MAXCT >= 4 ? 4 : 8;
   const int nct = N >> 4;
-  floatx4 acc[2][MAXCT];
+  floatx4 acc[RT][MAXCT];
 #pragma unroll
-  for (int c = 0; c < MAXCT; ++c) {
-    acc[0][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    acc[1][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  }
+  for (int c = 0; c < MAXCT; ++c)
+#pragma unroll
+    for (int r = 0; r < RT; ++r) acc[r][c] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int ka = lane >> 4;
   const int il = lane & 15;
-  const float* in0 = in + il * ldi + ka;
-  const float* in1 = in + (il + 16) * ldi + ka;
+  const float* inr[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) inr[r] = in + (il + 16 * r) * ldi + ka;
   const float* wb = W + (size_t)ka * N + il;
   for (int k0 = 0; k0 < K; k0 += 4 * U) {
-    float a0[U], a1[U], bf[U][MAXCT];
+    float av[RT][U], bf[U][MAXCT];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kk = k0 + 4 * u;
       const bool ok = kk < K;
-      a0[u] = ok ? in0[kk] : 0.f;
-      a1[u] = ok ? in1[kk] : 0.f;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) av[r][u] = ok ? inr[r][kk] : 0.f;
 #pragma unroll
       for (int c = 0; c < MAXCT; ++c) {
         const int ct = wave + c * 4;
@@ -516,8 +547,9 @@ __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi
 #pragma unroll
       for (int c = 0; c < MAXCT; ++c) {
         if (wave + c * 4 < nct) {
-          acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[u], bf[u][c], acc[0][c], 0, 0, 0);
-          acc[1][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u], bf[u][c], acc[1][c], 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r][u], bf[u][c], acc[r][c], 0, 0, 0);
         }
       }
     }
@@ -528,7 +560,7 @@ __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi
     if (ct < nct) {
       const int col = ct * 16 + il;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = rt * 16 + ka * 4 + j;
@@ -548,23 +580,20 @@ __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi
 }
 
 // Final Dense + softmax for row t (one thread), weights staged in LDS: ws[k*nout + c], wsb[c].
+// fp32 logits, softmax in fp64 rounded to fp32 (softmax_pick).
 __device__ __forceinline__ void last_layer_softmax(const float* in, int ldi, int K, int nout,
                                                    const float* ws, const float* wsb, int t,
                                                    float* prob) {
-  float mx = -__builtin_inff();
+  double z[8];
+  double mx = -__builtin_inf();
   for (int c = 0; c < nout; ++c) {
     float s = 0.f;
 #pragma unroll 8
     for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], ws[k * nout + c], s);
-    prob[c] = s + wsb[c];
-    mx = prob[c] > mx ? prob[c] : mx;
+    z[c] = (double)(s + wsb[c]);
+    mx = z[c] > mx ? z[c] : mx;
   }
-  float den = 0.f;
-  for (int c = 0; c < nout; ++c) {
-    prob[c] = expf(prob[c] - mx);
-    den += prob[c];
-  }
-  for (int c = 0; c < nout; ++c) prob[c] = prob[c] / den;
+  softmax_all(z, nout, mx, prob);
 }
 
 __host__ __device__ inline int max_hidden(const int* dims, int n_layers) {
@@ -789,20 +818,15 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     if (tid < M2_ROWS) {
       const int s = rowst[tid];
       if (s >= 0) {
-        float prob[8];
-        float mx = -__builtin_inff();
+        double z[8];
+        double mx = -__builtin_inf();
         for (int c = 0; c < nout; ++c) {
           const float* q = part + tid * nout + c;
-          prob[c] = (((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
-                     q[3 * M2_ROWS * nout]) + bl[c];
-          mx = prob[c] > mx ? prob[c] : mx;
+          z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
+                           q[3 * M2_ROWS * nout]) + bl[c]);
+          mx = z[c] > mx ? z[c] : mx;
         }
-        float den = 0.f;
-        for (int c = 0; c < nout; ++c) {
-          prob[c] = expf(prob[c] - mx);
-          den += prob[c];
-        }
-        const double f1 = (double)(prob[a.s.min_class[s]] / den);
+        const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
         const int i = r0 + tid - s * a.n;
         if (a.F) {
           const int orow = a.out_map ? a.out_map[(size_t)s * a.n + i] : i;
@@ -814,9 +838,10 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
   }
 }
 
-// Classifier.predict_proba: 32 rows per workgroup, full-width first layer.
-template <int MAXCT>
+// Classifier.predict_proba: 16 RT rows per workgroup, full-width first layer.
+template <int MAXCT, int RT = 2>
 __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
+  constexpr int TR = 16 * RT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nl = a.n_layers;
@@ -828,12 +853,12 @@ __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
   float* wsb = ws + Klast * nout;
   const size_t head = mlp_head_bytes(Klast, nout);
   float* R1 = (float*)(smem + head);
-  float* R2 = (float*)(smem + head + eval_region1_bytes(a.D4, hmax));
+  float* R2 = (float*)(smem + head + predict_region1_bytes(a.D4, hmax, TR));
   const int D = a.dims[0];
-  const int r0 = blockIdx.x * EVAL_TR;
+  const int r0 = blockIdx.x * TR;
   for (int q = tid; q < Klast * nout; q += EVAL_T) ws[q] = a.W[nl - 1][q];
   if (tid < nout) wsb[tid] = a.bias[nl - 1][tid];
-  for (int idx = tid; idx < EVAL_TR * a.D4; idx += EVAL_T) {
+  for (int idx = tid; idx < TR * a.D4; idx += EVAL_T) {
     const int t = idx / a.D4, j = idx - t * a.D4;
     const int r = r0 + t;
     R1[t * lda + j] = (r < a.n && j < D) ? (float)a.x[(size_t)r * D + j] : 0.f;
@@ -845,7 +870,7 @@ __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
   float* other = R1;
   for (int l = 0; l + 1 < nl; ++l) {
     const int N = a.dims[l + 1];
-    dense_mfma<MAXCT>(in, ldi, K, a.W[l], N, a.bias[l], nullptr, nullptr, outb, N + 1, wave,
+    dense_mfma<MAXCT, RT>(in, ldi, K, a.W[l], N, a.bias[l], nullptr, nullptr, outb, N + 1, wave,
                       lane);
     __syncthreads();
     in = outb;
@@ -855,7 +880,7 @@ __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
     outb = other;
     other = tmp;
   }
-  if (tid < EVAL_TR && r0 + tid < a.n) {
+  if (tid < TR && r0 + tid < a.n) {
     float prob[8];
     last_layer_softmax(in, ldi, K, nout, ws, wsb, tid, prob);
     for (int c = 0; c < nout; ++c) a.proba[(size_t)(r0 + tid) * nout + c] = (double)prob[c];
@@ -875,6 +900,43 @@ __global__ __launch_bounds__(256) void k_constraints(int slot, int n,
   for (int f = lane; f < p.D; f += 64) xrow[f] = x[(size_t)r * p.D + f];
   wave_sync();
   constraints_row<FULL>(global_tab(p), xrow, lane, G + (size_t)r * p.C, nullptr, false);
+}
+
+// FeatureEncoder.genetic_to_ml (feature_encoder.py:91-130) for host plugins: genes
+// [B][n][V] -> ML rows [B][n][D]; one thread per output feature (immutable features from
+// the state's x_init, one-hot features 1.0 where the group's gene equals their category).
+__global__ __launch_bounds__(256) void k_decode(const int* __restrict__ fdec,
+                                                const double* __restrict__ x_init, int B, int n,
+                                                int V, int D, const double* __restrict__ genes,
+                                                double* __restrict__ x) {
+  const long total = (long)B * n * D;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (long)gridDim.x * blockDim.x) {
+    const long row = t / D;
+    const int f = (int)(t - row * D);
+    const int b = (int)(row / n);
+    const int m = fdec[f];
+    double v;
+    if (m < 0) {
+      v = x_init[(size_t)b * D + f];
+    } else {
+      const double g = genes[(size_t)row * V + (m & 0xFFFF)];
+      const int cat = m >> 16;
+      v = cat ? (g == (double)(cat - 1) ? 1.0 : 0.0) : g;
+    }
+    x[t] = v;
+  }
+}
+
+hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, const double* genes,
+                         double* x, hipStream_t stream) {
+  const long total = (long)B * n * p.D;
+  if (total <= 0) return hipSuccess;
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(256), 0, stream, p.fdec, s.x_init, B,
+                     n, p.V, p.D, genes, x);
+  return hipGetLastError();
 }
 
 // Per-state constants: one workgroup per state.
@@ -968,8 +1030,6 @@ static void configure_lds_once() {
   const int lim = 160 * 1024;
   const void* fns[] = {(const void*)k_mlp<1>,          (const void*)k_mlp<2>,
                        (const void*)k_mlp<4>,          (const void*)k_mlp<8>,
-                       (const void*)k_predict<1>,      (const void*)k_predict<2>,
-                       (const void*)k_predict<4>,      (const void*)k_predict<8>,
                        (const void*)k_constraints<false>, (const void*)k_constraints<true>};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -1078,8 +1138,59 @@ hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t s
 #undef CONS
 }
 
+template <bool IDENT, int NT, bool FULL>
+static hipError_t rows_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_rows<IDENT, NT, FULL>);
+    configured = true;
+  }
+  hipLaunchKernelGGL((k_rows<IDENT, NT, FULL>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  return hipGetLastError();
+}
+
+size_t rows_fused_lds(const DProblem& p) { return fused_lds(vary_offsets(p), VARY_T / 64).total; }
+
+hipError_t launch_rows_fused(const RowsArgs& a, int slot, int gen, int hist_row0,
+                             hipStream_t stream) {
+  if (a.total <= 0) return hipSuccess;
+  const int B = a.total / a.n;
+  const int rw = vary_rows_per_wg(a.n);
+  const dim3 grid(B * ((a.n + rw - 1) / rw));
+  const int nt = vary_nt(a.p);
+  const size_t lds = rows_fused_lds(a.p);
+#define RW(I, N, F) return rows_go<I, N, F>(grid, lds, stream, slot, gen, hist_row0, rw)
+  if (a.p.ident) {
+    if (nt == 1) RW(true, 1, false);
+    if (nt == 2) RW(true, 2, false);
+    if (nt == 4) RW(true, 4, false);
+    if (nt == 8) RW(true, 8, false);
+    RW(true, 16, false);
+  }
+  if (a.p.full_ops) {
+    if (nt == 1) RW(false, 1, true);
+    if (nt == 2) RW(false, 2, true);
+    if (nt == 4) RW(false, 4, true);
+    if (nt == 8) RW(false, 8, true);
+    RW(false, 16, true);
+  }
+  if (nt == 1) RW(false, 1, false);
+  if (nt == 2) RW(false, 2, false);
+  if (nt == 4) RW(false, 4, false);
+  if (nt == 8) RW(false, 8, false);
+  RW(false, 16, false);
+#undef RW
+}
+
+// Variation + evaluation of the rows in the per-phase chain: k_gen then k_cons.  (The fused
+// k_rows was measured slower here -- 2 workgroups per CU instead of 4 hide less of the
+// per-row latency -- and with several state-group streams it showed rare run-to-run
+// differences that were not found; it is kept for MV_ROWS_FUSED experiments only.  Its body
+// is the whole-attack kernel's row phase, which is deterministic and tested.)
 hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream) {
+  if (a.do_eval && rows_fused_lds(a.p) <= 160 * 1024 && std::getenv("MV_ROWS_FUSED"))
+    return launch_rows_fused(a, slot, gen, hist_row0, stream);
   hipError_t e = launch_gen(a, slot, gen, hist_row0, stream);
   if (e != hipSuccess) return e;
   return launch_cons(a, slot, hist_row0, stream);
@@ -1123,7 +1234,7 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
 }
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
-  if (a.total <= 0) return hipSuccess;
+  if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
   if (a.p.mlp2 && !std::getenv("MV_MLP_V1"))
     return mlp2_hmax(a.p) <= 64 ? mlp2_go<1>(a, slot, hist_row0, stream)
                                 : mlp2_go<2>(a, slot, hist_row0, stream);
@@ -1151,23 +1262,39 @@ hipError_t launch_rows(const RowsArgs& a, int slot, int gen, int hist_row0,
   return launch_mlp(a, slot, hist_row0, stream);
 }
 
+template <int RT>
+static hipError_t predict_go(const MlpArgs& a, int nct, size_t lds, hipStream_t stream) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_predict<1, RT>);
+    allow_lds(k_predict<2, RT>);
+    allow_lds(k_predict<4, RT>);
+    allow_lds(k_predict<8, RT>);
+    configured = true;
+  }
+  const dim3 grid((a.n + 16 * RT - 1) / (16 * RT));
+  if (nct <= 4)
+    hipLaunchKernelGGL((k_predict<1, RT>), grid, dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 8)
+    hipLaunchKernelGGL((k_predict<2, RT>), grid, dim3(EVAL_T), lds, stream, a);
+  else if (nct <= 16)
+    hipLaunchKernelGGL((k_predict<4, RT>), grid, dim3(EVAL_T), lds, stream, a);
+  else
+    hipLaunchKernelGGL((k_predict<8, RT>), grid, dim3(EVAL_T), lds, stream, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream) {
   if (a.n <= 0) return hipSuccess;
-  configure_lds_once();
   const int nl = a.n_layers;
   const int hmax = max_hidden(a.dims, nl);
-  const size_t lds = mlp_lds_bytes(a.D4, hmax, a.dims[nl - 1], a.dims[nl]);
-  const dim3 grid((a.n + EVAL_TR - 1) / EVAL_TR);
   const int nct = hmax / 16;
-  if (nct <= 4)
-    hipLaunchKernelGGL(k_predict<1>, grid, dim3(EVAL_T), lds, stream, a);
-  else if (nct <= 8)
-    hipLaunchKernelGGL(k_predict<2>, grid, dim3(EVAL_T), lds, stream, a);
-  else if (nct <= 16)
-    hipLaunchKernelGGL(k_predict<4>, grid, dim3(EVAL_T), lds, stream, a);
-  else
-    hipLaunchKernelGGL(k_predict<8>, grid, dim3(EVAL_T), lds, stream, a);
-  return hipGetLastError();
+  // 32-row tiles when they fit the LDS, else 16-row tiles (e.g. 756-512-... models)
+  const size_t lds32 = predict_lds_bytes(a.D4, hmax, a.dims[nl - 1], a.dims[nl], 32);
+  if (lds32 <= 160 * 1024) return predict_go<2>(a, nct, lds32, stream);
+  const size_t lds16 = predict_lds_bytes(a.D4, hmax, a.dims[nl - 1], a.dims[nl], 16);
+  if (lds16 > 160 * 1024) return hipErrorInvalidValue;
+  return predict_go<1>(a, nct, lds16, stream);
 }
 
 hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double* x,

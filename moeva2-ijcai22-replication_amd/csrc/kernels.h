@@ -26,13 +26,14 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
 // Problem and per-state blobs: HBM images of LDS regions, each region 1-KiB aligned so a
 // workgroup stages the regions it needs with 16-B-per-lane global_load_lds copies.
 //   problem blob  A: constraint program (opa, opk, opc, ocol, pool)       -> k_cons
-//                 B: mutation gap table, gene table, mutable features     -> k_gen
+//                 B: mutation gap table, gene table, mutable features,
+//                    one-hot group offsets / features                     -> k_gen
 //                 C: ML scaler at the mutable features (mlS, mlM)         -> k_gen
 //   state blob    X: x_init                                               -> k_cons (k_gen OHE)
 //                 E: encoder MinMax at the mutable features (es, em, x0)  -> k_gen
 struct VaryOff {
   unsigned opa, opk, opc, ocol, pool, a_end;      // region A at 0
-  unsigned geo, ginfo, mutf, b_at, b_end;         // region B at b_at
+  unsigned geo, ginfo, mutf, ooff, ofeat, b_at, b_end;  // region B at b_at
   unsigned mlS, mlM, c_at, vb;                    // region C at c_at; vb = blob bytes
   unsigned xi, x_end;                             // region X at 0
   unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
@@ -59,6 +60,8 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   o.geo = take((size_t)(p.V + 1) * 4);
   o.ginfo = take((size_t)((p.V + 3) & ~3) * 4);
   o.mutf = take(Dm4 * 4);
+  o.ooff = take((size_t)(p.n_ohe + 1) * 4);
+  o.ofeat = take((size_t)(p.n_ohe_feat > 0 ? p.n_ohe_feat : 1) * 4);
   o.b_end = kb(off);
   o.c_at = o.b_end;
   off = o.c_at;
@@ -112,13 +115,16 @@ __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + (VARY_T / 64) * o.rb;
 }
 
-// fused row phase of the whole-attack kernel: regions B, C, E, then one D-wide row per wave
+// fused row kernel (k_rows, whole-attack rows phase): regions A, B, C, E, then one D-wide
+// row per wave
 struct FusedLds {
-  unsigned b_at, c_at, e_at, rows_at, total;
+  unsigned a_at, b_at, c_at, e_at, rows_at, total;
 };
 __host__ __device__ inline FusedLds fused_lds(const VaryOff& o, int waves) {
   FusedLds l{};
   unsigned at = 0;
+  l.a_at = at;
+  at += o.a_end;
   l.b_at = at;
   at += o.b_end - o.b_at;
   l.c_at = at;
@@ -131,7 +137,21 @@ __host__ __device__ inline FusedLds fused_lds(const VaryOff& o, int waves) {
   return l;
 }
 
+// k_predict: TR-row tiles (32, or 16 for inputs too wide for a 32-row tile)
+__host__ __device__ inline size_t predict_region1_bytes(int D4, int hmax, int TR) {
+  const size_t a = (size_t)TR * (D4 + 1) * sizeof(float);
+  const size_t h = (size_t)TR * (hmax + 1) * sizeof(float);
+  const size_t r = a > h ? a : h;
+  return (r + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t predict_lds_bytes(int D4, int hmax, int Klast, int nout, int TR) {
+  return mlp_head_bytes(Klast, nout) + predict_region1_bytes(D4, hmax, TR) +
+         (size_t)TR * (hmax + 1) * sizeof(float);
+}
+
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
+hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, const double* genes,
+                         double* x, hipStream_t stream);
 size_t attack_lds_bytes(const DProblem& p, int P, int O, int R, int T);
 bool attack_supported(const DProblem& p, int P, int O, int R);
 hipError_t launch_attack(const AttackArgs& args, hipStream_t stream);

@@ -21,6 +21,7 @@ enum : uint32_t {
   TAG_MUT_U = 5,
   TAG_NICHE_PERM = 6,
   TAG_NICHE_MEMBER = 7,
+  TAG_SBX = 8,
 };
 
 struct u32x4 {

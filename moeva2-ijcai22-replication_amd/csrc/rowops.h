@@ -269,6 +269,20 @@ __device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restri
   }
 }
 
+// scatter_gene with the one-hot tables in LDS (region B)
+__device__ __forceinline__ void scatter_gene_tab(const int* __restrict__ ooff,
+                                                 const int* __restrict__ ofeat,
+                                                 double* __restrict__ xrow, int info, double x) {
+  const int kind = info & 3;
+  const int feat = (info >> 17) & 0x7FFF;
+  if (kind != 2) {
+    xrow[feat] = x;
+  } else {
+    const int o0 = ooff[feat], o1 = ooff[feat + 1];
+    for (int k = o0; k < o1; ++k) xrow[ofeat[k]] = (x == (double)(k - o0)) ? 1.0 : 0.0;
+  }
+}
+
 __device__ __forceinline__ int rdl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
 // Geometric gap of the mutation process (oracle mutation_draws): the number of
@@ -281,6 +295,29 @@ __device__ __forceinline__ int geo_gap(const uint32_t* T, int V, uint32_t w, flo
   while (k < V && w < T[k + 1]) ++k;
   while (k > 0 && !(w < T[k])) --k;
   return k;
+}
+
+// pymoo 0.4.2.2 SimulatedBinaryCrossover._do for one gene of one mating [pymoo-recall;
+// SURVEY.md §7 "north_star says SBX"]: the child of `side` (0: c[0], 1: c[1]) from parents
+// p0 = X[0], p1 = X[1] with bounds [xl, xu] (widened for integer genes by the caller), the
+// uniform `rand` of calc_betaq and the swap draw; numpy's evaluation order, no FMA.
+__device__ __forceinline__ double sbx_child(double p0, double p1, double xl, double xu,
+                                            double rand, bool swap, int side, double eta) {
+  const double y1 = p0 < p1 ? p0 : p1;
+  const double y2 = p0 < p1 ? p1 : p0;
+  double delta = y2 - y1;
+  if (delta < 1.0e-10) delta = 1.0e-10;
+  // c[0] takes c1 (lower side) unless swapped; c[1] the other one
+  const bool low = (side == 0) != swap;
+  const double beta = low ? 1.0 + (2.0 * (y1 - xl) / delta) : 1.0 + (2.0 * (xu - y2) / delta);
+  const double alpha = 2.0 - pow(beta, -(eta + 1.0));
+  const double ex = 1.0 / (eta + 1.0);
+  const double betaq =
+      rand <= (1.0 / alpha) ? pow((rand * alpha), ex) : pow((1.0 / (2.0 - rand * alpha)), ex);
+  double c = low ? 0.5 * ((y1 + y2) - betaq * delta) : 0.5 * ((y1 + y2) + betaq * delta);
+  if (c < xl) c = xl;  // set_to_bounds_if_outside_by_problem
+  if (c > xu) c = xu;
+  return c;
 }
 
 // MixedVariableMutation of one gene (moeva2.py:104-111): real_pm, or int_pm =
@@ -296,14 +333,75 @@ __device__ __forceinline__ double mutate_gene(double x, double xl, double xu, bo
   return yi;
 }
 
+constexpr int MUT_CAP = 4;     // mutations per row precomputed in the prologue (registers)
+constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream (V <= 1024)
+
+// SBX option of the mixed-variable crossover (real_sbx / int_sbx = IntegerFromFloat-
+// Crossover(SBX): widened bounds, np.round, then the build's clamp to [xl, xu]) for one row
+// whose genes lane + 64 t hold the row's own parent.  Mating m's draws per gene g: one
+// Philox word (index m * MUT_J + g, TAG_SBX): bit 0 = 0 -> the variable crosses
+// (prob_per_variable 0.5), bit 1 -> swap c1/c2, words y, z -> calc_betaq's uniform.  The
+// mating-level draw (prob 0.9) of each subset comes from TAG_CX as for two-point.
+template <int NT>
+__device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double* goth,
+                                        const double* gl, const double* gu, int V, int m,
+                                        int side, int on0, int on1, const Rng& rng, int gen,
+                                        double eta, int lane) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int g = lane + 64 * t;
+    if (g >= V) continue;
+    const bool real = (ginf[t] & 3) == 0;
+    if (!(real ? on0 : on1)) continue;
+    const double own = x[t], oth = goth[g];
+    const double p0 = side == 0 ? own : oth, p1 = side == 0 ? oth : own;
+    const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
+    if ((w.x & 1u) || !(fabs(p0 - p1) > 1.0e-14)) continue;
+    const double lo = gl[g], hi = gu[g];
+    double c = sbx_child(p0, p1, real ? lo : lo - INT_WIDEN, real ? hi : hi + INT_WIDEN,
+                         u53(w.y, w.z), (w.x & 2u) != 0u, side, eta);
+    if (!real) {
+      c = rint(c);
+      if (c < lo) c = lo;
+      if (c > hi) c = hi;
+    }
+    x[t] = c;
+  }
+}
+
+// Every mutation of row i (the whole geometric-gap draw sequence of mutation_draws, no
+// register cache): the SBX rows take this path since their crossed values exist only in the
+// row loop.
+template <int NT>
+__device__ __forceinline__ void mutate_row_full(double* x, const uint32_t* s_geo,
+                                                const int* s_ginfo, const double* gl,
+                                                const double* gu, int V, int i, const Rng& rng,
+                                                int gen, double eta, int lane) {
+  const float lq = __log2f(1.0f - 1.0f / (float)V);
+  int pos = -1;
+  for (int j = 0;; ++j) {
+    const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+    pos += 1 + geo_gap(s_geo, V, w.x, lq);
+    if (pos >= V) break;
+    if ((pos & 63) == lane) {
+      double xv = 0.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (pos == lane + 64 * t) xv = x[t];
+      xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), eta);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (pos == lane + 64 * t) x[t] = xv;
+    }
+  }
+}
+
 __device__ __forceinline__ bool gene_swapped(int info, int on0, int lo0, int hi0, int on1,
                                              int lo1, int hi1) {
   const int sub = (info >> 2) & 0x7FFF;
   return (info & 3) == 0 ? (on0 && sub >= lo0 && sub < hi0) : (on1 && sub >= lo1 && sub < hi1);
 }
 
-constexpr int MUT_CAP = 4;     // mutations per row precomputed in the prologue (registers)
-constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream (V <= 1024)
 
 // Crossover draws of one subset packed into one word: on | lo << 1 | hi << 16.
 __device__ __forceinline__ int pack_cx(const CxSub& c) { return c.on | (c.lo << 1) | (c.hi << 16); }
@@ -318,13 +416,41 @@ __device__ __forceinline__ double rdl_d(double v, int k) {
   return __hiloint2double(hi, lo);
 }
 
+// Softmax of fp32 logits z[0..nout) (as fp64, with their max mx) -> probability of class c,
+// computed in fp64 and rounded to fp32 (Keras returns fp32).  exp() in fp64 and a single
+// final rounding make the value a function of the logits alone -- independent of the expf
+// implementation -- so a CPU restatement reproduces it bit for bit
+// (oracle/device_order.py); it is within an fp32 ulp of Keras' fp32 softmax.
+// z is overwritten with the exponentials; softmax_all writes every class's probability.
+__device__ __forceinline__ double softmax_pick(double* z, int nout, double mx, int c) {
+  double den = 0.0;
+  for (int k = 0; k < nout; ++k) {
+    z[k] = exp(z[k] - mx);
+    den = den + z[k];
+  }
+  return (double)(float)(z[c] / den);
+}
+__device__ __forceinline__ void softmax_all(double* z, int nout, double mx, float* prob) {
+  double den = 0.0;
+  for (int k = 0; k < nout; ++k) {
+    z[k] = exp(z[k] - mx);
+    den = den + z[k];
+  }
+  for (int k = 0; k < nout; ++k) prob[k] = (float)(z[k] / den);
+}
+
 // Async global -> LDS copy of nbytes (a 1-KiB multiple): 16 B per lane, 1 KiB per wave
 // instruction, the workgroup's waves interleaved.
 template <int T = VARY_T>
 __device__ __forceinline__ void glds_copy(unsigned char* lds, const unsigned char* g,
                                           unsigned nbytes, int wave, int lane) {
+#ifdef MV_NO_LDS_DMA
+  for (unsigned off = wave * 1024u; off < nbytes; off += T * 16u)
+    *(uint4*)(lds + off + lane * 16) = *(const uint4*)(g + off + lane * 16);
+#else
   for (unsigned off = wave * 1024u; off < nbytes; off += T * 16u)
     __builtin_amdgcn_global_load_lds(g + off + lane * 16, lds + off, 16, 0, 0);
+#endif
 }
 
 // Rows of one k_gen / k_cons workgroup: a chunk of one state's rows; wave w takes rows

@@ -22,9 +22,10 @@ OP = dict(DIFF=1, RATIO_SAFE=2, ABS_SUMDIFF=3, LCLD_INSTALL=4, LCLD_TERM=5, ABS_
 
 EXPORTED = [
     "mv_last_error", "mv_device_count", "mv_engine_create", "mv_engine_destroy",
-    "mv_set_states", "mv_evaluate", "mv_constraints", "mv_survive", "mv_select_parents",
+    "mv_set_states", "mv_evaluate", "mv_decode", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
     "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_set_attack_mode",
+    "mv_set_crossover",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
 ]
@@ -86,6 +87,7 @@ def lib():
                                  C.POINTER(vp)],
             "mv_set_states": [vp, C.c_int32, _f64p, _f64p, _f64p, _i32p, vp],
             "mv_evaluate": [vp, C.c_int32, vp, vp, vp, vp],
+            "mv_decode": [vp, C.c_int32, vp, vp, vp],
             "mv_constraints": [vp, C.c_int32, vp, vp, vp],
             "mv_survive": [C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_double,
                            C.c_uint64, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -98,6 +100,7 @@ def lib():
             "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
             "mv_get_phase_times": [vp, _f64p, _i32p],
             "mv_set_attack_mode": [vp, C.c_int32],
+            "mv_set_crossover": [vp, C.c_int32, C.c_double, C.c_double],
             "mv_get_attack_time": [vp, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
@@ -248,7 +251,10 @@ class Engine:
             self._h = None
 
     # -- per-state constants
-    def set_states(self, x_init, xl, xu, minimize_class, stream=None):
+    def set_states(self, x_init, xl, xu, minimize_class, stream=None, owner=None):
+        """Bind B initial states (mv_set_states).  ``owner`` tags the binding so a caller
+        that evaluates repeatedly on the same states (DefaultProblem) binds only once."""
+        self.bound_by = owner
         x_init = _arr(x_init, np.float64)
         xl = _arr(xl, np.float64)
         xu = _arr(xu, np.float64)
@@ -263,6 +269,10 @@ class Engine:
         """genes (B, n, V) fp64 device tensor -> F (B, n, 3) [, G (B, n, C)]."""
         check(lib().mv_evaluate(self._h, genes.shape[1], _ptr(genes), _ptr(F), _ptr(G),
                                 _stream(stream)))
+
+    def decode(self, genes, x, stream=None):
+        """genes (B, n, V) -> ML-space rows x (B, n, D) (FeatureEncoder.genetic_to_ml)."""
+        check(lib().mv_decode(self._h, genes.shape[1], _ptr(genes), _ptr(x), _stream(stream)))
 
     def constraints(self, x, G, stream=None):
         """x (n, D) fp64 device tensor -> G (n, C) (the numpy-path Constraints.evaluate)."""
@@ -289,10 +299,16 @@ class Engine:
     def set_profiling(self, on: bool):
         check(lib().mv_set_profiling(self._h, int(on)))
 
+    def set_crossover(self, kind: str = "two_point", eta: float = 30.0, prob: float = 0.9):
+        """"two_point" (the reference's operator) or "sbx" (SimulatedBinaryCrossover)."""
+        check(lib().mv_set_crossover(self._h, {"two_point": 0, "sbx": 1}[kind], float(eta),
+                                     float(prob)))
+
     def set_attack_mode(self, mode: str):
-        """"auto": the whole-attack kernel when the problem shape has an instance (default);
-        "chain": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per generation)."""
-        check(lib().mv_set_attack_mode(self._h, {"auto": 0, "chain": 1}[mode]))
+        """"chain": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per
+        generation); "whole": one k_attack launch for the whole attack (one workgroup per
+        state) when the problem layout has an instance; "auto" (default): the faster one."""
+        check(lib().mv_set_attack_mode(self._h, {"auto": 0, "chain": 1, "whole": 2}[mode]))
 
     def attack_time(self):
         """(device ms of the last profiled whole-attack launch, whether it ran as one launch)."""

@@ -7,6 +7,7 @@ program all execute in one HIP kernel.
 """
 import numpy as np
 
+from ...hosted import HostPlugins
 from ...problem import get_engine
 from .classifier import Classifier
 from .constraints import Constraints
@@ -42,6 +43,7 @@ class DefaultProblem:
         self.n_constr = 0
         self._engine = get_engine(constraints, classifier, ml_scaler, norm, scale_objectives,
                                   device)
+        self._plugins = HostPlugins(constraints, classifier, ml_scaler)
         xl_f, xu_f = constraints.get_feature_min_max(dynamic_input=self.x_initial_ml)
         self._bind = (self.x_initial_ml[None, :], np.asarray(xl_f, np.float64)[None, :],
                       np.asarray(xu_f, np.float64)[None, :], np.array([minimize_class]))
@@ -62,13 +64,19 @@ class DefaultProblem:
         if (x - self.xl < 0).sum() > 0 or (x - self.xu > 0).sum() > 0:
             print("Lower than lower bound.")  # default_problem.py:102-106
         eng = self._engine
-        eng.set_states(*self._bind)
+        if getattr(eng, "bound_by", None) is not self:  # bind once, re-bind only if the
+            eng.set_states(*self._bind, owner=self)     # shared engine was rebound since
         genes = torch.from_numpy(x).cuda()[None]
         F = torch.empty((1, x.shape[0], 3), dtype=torch.float64, device=genes.device)
         full = isinstance(self._save_history, str) and "full" in self._save_history
+        host_g = full and self._plugins.host_constraints
         G = (torch.empty((1, x.shape[0], eng.prog.C), dtype=torch.float64, device=genes.device)
-             if full else None)
+             if full and not host_g else None)
         eng.evaluate(genes, F, G)
+        Gh = [] if host_g else None
+        self._plugins.fill(eng, genes, F, [self.minimize_class], Gh)  # host plugins, if any
+        if host_g:
+            G = torch.as_tensor(Gh[0])
         out["F"] = F[0].cpu().numpy()
         self.nb_eval += x.shape[0]
         if isinstance(self._save_history, str) and "reduced" in self._save_history:

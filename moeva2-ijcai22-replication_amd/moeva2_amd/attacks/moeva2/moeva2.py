@@ -11,6 +11,7 @@ import secrets
 
 import numpy as np
 
+from ...hosted import HostPlugins, hosted_attack
 from ...problem import get_engine
 from .classifier import Classifier, load_model
 from .constraints import Constraints
@@ -46,7 +47,8 @@ class Moeva2:
     def __init__(self, classifier_path: str, constraints: Constraints, ml_scaler=None,
                  problem_class=None, l2_ball_size=0.1, norm=np.inf, n_gen=625, n_pop=640,
                  n_offsprings=320, scale_objectives=True, save_history=False, seed=None,
-                 n_jobs=-1, verbose=1, device: int = 0) -> None:
+                 n_jobs=-1, verbose=1, device: int = 0, crossover: str = "two_point",
+                 sbx_eta: float = 30.0) -> None:
         self._classifier_path = classifier_path
         self._constraints = constraints
         self._ml_scaler = ml_scaler
@@ -63,6 +65,13 @@ class Moeva2:
         self.l2_ball_size = l2_ball_size
         self.norm = norm
         self.device = device
+        # engine extension: "two_point" = the reference's operator (moeva2.py:90-101);
+        # "sbx" = SimulatedBinaryCrossover (north_star; the stale moeva2.py:87 comment's
+        # prob 0.9, eta 30)
+        if crossover not in ("two_point", "sbx"):
+            raise ValueError(f"crossover must be 'two_point' or 'sbx', got {crossover!r}")
+        self._crossover = crossover
+        self._sbx_eta = sbx_eta
         self._classifier = None
         self.last_engine = None
 
@@ -97,8 +106,10 @@ class Moeva2:
         B = x.shape[0]
         if B == 0:  # the reference's list comprehension over no states
             return self._empty_device() + (None,) if return_device else []
-        eng = get_engine(self._constraints, self._get_classifier(), self._ml_scaler, self.norm,
+        clf = self._get_classifier()
+        eng = get_engine(self._constraints, clf, self._ml_scaler, self.norm,
                          self._scale_objectives, self.device)
+        eng.set_crossover(self._crossover, self._sbx_eta)
         bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
         xl = np.array([b[0] for b in bounds], np.float64)
         xu = np.array([b[1] for b in bounds], np.float64)
@@ -107,17 +118,27 @@ class Moeva2:
         seed = self._seed if self._seed is not None else secrets.randbits(63)
         ref = energy_ref_dirs(N_OBJ, self._n_pop, seed=1)
         hmode = history_mode(self._save_history)
-        eng.attack_run(self._n_gen, P, O, int(seed), ref, MU, hmode)
-        V = eng.prog.V
-        dev = torch.device("cuda", self.device)
-        genes = torch.empty((B, P, V), dtype=torch.float64, device=dev)
-        F = torch.empty((B, P, 3), dtype=torch.float64, device=dev)
-        eng.attack_population(genes, F)
-        hist = None
-        if hmode:
-            w = 3 if hmode == 1 else 3 + eng.prog.C
-            hist = torch.empty((B, P + (self._n_gen - 1) * O, w), dtype=torch.float64, device=dev)
-            eng.attack_history(hist)
+        plugins = HostPlugins(self._constraints, clf, self._ml_scaler)
+        if plugins.any:
+            # a plugin the engine cannot compile: host-driven loop around device calls
+            g0 = self._encoder.ml_to_genetic(x)
+            nonreal = np.asarray([t != "real" for t in self._encoder.get_type_mask_genetic()])
+            g0[:, nonreal] = np.rint(g0[:, nonreal])
+            genes, F, hist = hosted_attack(eng, plugins, g0, minimize_class, self._n_gen, P, O,
+                                           int(seed), ref, MU, hmode)
+        else:
+            eng.attack_run(self._n_gen, P, O, int(seed), ref, MU, hmode)
+            V = eng.prog.V
+            dev = torch.device("cuda", self.device)
+            genes = torch.empty((B, P, V), dtype=torch.float64, device=dev)
+            F = torch.empty((B, P, 3), dtype=torch.float64, device=dev)
+            eng.attack_population(genes, F)
+            hist = None
+            if hmode:
+                w = 3 if hmode == 1 else 3 + eng.prog.C
+                hist = torch.empty((B, P + (self._n_gen - 1) * O, w), dtype=torch.float64,
+                                   device=dev)
+                eng.attack_history(hist)
         self.last_engine = eng
         if return_device:
             return genes, F, hist

@@ -771,6 +771,77 @@ def crossover(parents_X, masks_by_type, seed, gen, stream_key=0):
     return out.reshape(-1, V)
 
 
+def sbx_draws(n_matings, V, seed, gen, stream_key=0):
+    """Philox statement of SimulatedBinaryCrossover's per-variable draws [pymoo-recall]:
+    one word per (mating m, gene g) at index m*MUT_J + g, TAG_SBX: bit 0 == 0 -> the
+    variable crosses (``random > prob_per_variable`` with prob 0.5), bit 1 -> swap c1/c2
+    (``random <= 0.5``), words 1, 2 -> calc_betaq's uniform ``rand``."""
+    st = px.Stream(seed, gen, px.TAG_SBX, stream_key)
+    idx = (np.arange(n_matings, dtype=np.int64)[:, None] * MUT_J +
+           np.arange(V, dtype=np.int64)[None, :])
+    w0, w1, w2, _ = st.words(idx)
+    return (w0 & 1) == 0, (w0 & 2) != 0, px.u53(w1, w2)
+
+
+def sbx_pair(p0, p1, xl, xu, rand, swap, eta):
+    """pymoo 0.4.2.2 SimulatedBinaryCrossover._do [pymoo-recall] on aligned arrays: the two
+    children (c[0], c[1]) where every variable crosses (the caller masks), clipped to the
+    bounds (set_to_bounds_if_outside_by_problem)."""
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        y1 = np.minimum(p0, p1)
+        y2 = np.maximum(p0, p1)
+        delta = y2 - y1
+        delta = np.where(delta < 1.0e-10, 1.0e-10, delta)
+
+        def calc_betaq(beta):
+            alpha = 2.0 - np.power(beta, -(eta + 1.0))
+            mask = rand <= (1.0 / alpha)
+            return np.where(mask, np.power((rand * alpha), (1.0 / (eta + 1.0))),
+                            np.power((1.0 / (2.0 - rand * alpha)), (1.0 / (eta + 1.0))))
+
+        beta = 1.0 + (2.0 * (y1 - xl) / delta)
+        c1 = 0.5 * ((y1 + y2) - calc_betaq(beta) * delta)
+        beta = 1.0 + (2.0 * (xu - y2) / delta)
+        c2 = 0.5 * ((y1 + y2) + calc_betaq(beta) * delta)
+    a, b = np.where(swap, c2, c1), np.where(swap, c1, c2)
+    a = np.minimum(np.maximum(a, xl), xu)
+    b = np.minimum(np.maximum(b, xl), xu)
+    return a, b
+
+
+def sbx_crossover(parents_X, masks_by_type, xl, xu, seed, gen, eta=30.0, prob=0.9,
+                  stream_key=0):
+    """MixedVariableCrossover with real_sbx / int_sbx (north_star's SBX option; the
+    reference's stale comment moeva2.py:87 names prob 0.9, eta 30): per subset the
+    mating-level draw of crossover_draws (prob), then SBX per variable; int_sbx =
+    IntegerFromFloatCrossover [pymoo-recall]: bounds widened by 0.5-1e-16, np.round, and
+    the build's clamp to [xl, xu] (as for the mutation).  parents_X: (2, n_matings, V)."""
+    X = np.array(parents_X, dtype=np.float64, copy=True)
+    _, n_m, V = X.shape
+    out = X.copy()
+    var_on, swap, rand = sbx_draws(n_m, V, seed, gen, stream_key)
+    xl = np.asarray(xl, np.float64)
+    xu = np.asarray(xu, np.float64)
+    for subset, mask in enumerate(masks_by_type):
+        idx = np.where(mask)[0]
+        if idx.size == 0:
+            continue
+        do, _ = crossover_draws(idx.size, n_m, subset, seed, gen, stream_key, prob)
+        p0, p1 = X[0][:, idx], X[1][:, idx]
+        lo, hi = xl[idx][None, :], xu[idx][None, :]
+        wl, wu = (lo, hi) if subset == 0 else (lo - INT_WIDEN, hi + INT_WIDEN)
+        c0, c1 = sbx_pair(p0, p1, wl, wu, rand[:, idx], swap[:, idx], eta)
+        cross = var_on[:, idx] & (np.abs(p0 - p1) > 1.0e-14) & do[:, None]
+        c0 = np.where(cross, c0, p0)
+        c1 = np.where(cross, c1, p1)
+        if subset == 1:
+            c0 = np.minimum(np.maximum(np.round(c0), lo), hi)
+            c1 = np.minimum(np.maximum(np.round(c1), lo), hi)
+        out[0][:, idx] = c0
+        out[1][:, idx] = c1
+    return out.reshape(-1, V)
+
+
 def polynomial_mutation(X, xl, xu, eta, do_mutation, rand):
     """softmax_mutation.py:60-108 (pymoo PolynomialMutation._do) without the softmax.
     ``do_mutation`` (n, V) bool and ``rand`` (n_mutated,) are the two np.random draws."""
@@ -885,13 +956,17 @@ def initial_population(prob: Problem, pop_size: int) -> np.ndarray:
 
 
 def run_attack(prob: Problem, ref_points, n_gen, pop_size, n_offsprings, seed, mu=0.05,
-               save_history=None, stream_key=0):
+               save_history=None, stream_key=0, crossover_kind="two_point", sbx_eta=30.0,
+               evaluate_fn=None):
+    """evaluate_fn(prob, genes, return_g=True) -> (F, G): default ``evaluate`` (numpy's
+    summation orders); oracle.device_order.evaluate_device_order gives the engine's."""
+    evaluate_fn = evaluate_fn or evaluate
     asp = np.full((1, 3), 1.0 / 3.0)
     gl, gu = genetic_bounds(prob.lay, prob.xl, prob.xu)
     types = genetic_types(prob.lay)
     masks = [np.array([t == "real" for t in types]), np.array([t == "int" for t in types])]
     X = initial_population(prob, pop_size)
-    F, G = evaluate(prob, X, return_g=True)
+    F, G = evaluate_fn(prob, X, return_g=True)
     hist = []
     _hist_add(hist, save_history, F, G)
     st = SurvivalState()
@@ -900,9 +975,13 @@ def run_attack(prob: Problem, ref_points, n_gen, pop_size, n_offsprings, seed, m
     for g in range(1, n_gen):
         par = tournament_parents(X.shape[0], n_offsprings, seed, g, stream_key)
         pX = np.stack([X[par[:, 0]], X[par[:, 1]]])
-        off = crossover(pX, masks, seed, g, stream_key)[:n_offsprings]
+        if crossover_kind == "sbx":
+            off = sbx_crossover(pX, masks, gl, gu, seed, g, sbx_eta, 0.9, stream_key)
+        else:
+            off = crossover(pX, masks, seed, g, stream_key)
+        off = off[:n_offsprings]
         off = mutation(off, gl, gu, types, seed, g, stream_key=stream_key)
-        Fo, Go = evaluate(prob, off, return_g=True)
+        Fo, Go = evaluate_fn(prob, off, return_g=True)
         _hist_add(hist, save_history, Fo, Go)
         mX = np.concatenate([X, off])
         mF = np.concatenate([F, Fo])

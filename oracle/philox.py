@@ -32,6 +32,7 @@ TAG_MUT_MASK = 4
 TAG_MUT_U = 5
 TAG_NICHE_PERM = 6
 TAG_NICHE_MEMBER = 7
+TAG_SBX = 8
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):

@@ -1,0 +1,100 @@
+"""End-to-end parity at the benchmark configurations (north_star: the constrained attack
+success rate within 1 pp of the reference on the same initial states and budgets).
+
+The reference's pymoo/TensorFlow path cannot run here, so the end-to-end oracle is the CPU
+restatement's attack (oracle.moeva_oracle.run_attack) on the same states, budget and seed,
+committed as fixtures by tests/golden/make_e2e.py (387 botnet states x 1000 generations
+took ~50 CPU-core-minutes per 100 states).  Both sides are scored with the oracle's
+ObjectiveCalculator restatement (objective_calculator.py:44-119, 04_moeva.py:112-131).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import RES
+from oracle import moeva_oracle as mo
+from oracle.problems import PROJECTS, Project
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+class NpScaler:
+    def __init__(self, path):
+        d = np.load(path)
+        self.scale_, self.min_ = d["scale_"], d["min_"]
+
+
+def _device_attack(name, X, n_gen, n_pop, n_off, seed):
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, load_model
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+    from moeva2_amd.experiments.united.utils import STR_TO_CONSTRAINTS_CLASS
+    from moeva2_amd.problem import get_engine
+
+    feat = os.path.join(RES, PROJECTS[name][0])
+    c = STR_TO_CONSTRAINTS_CLASS[name](feat, feat.replace("features", "constraints"))
+    clf = Classifier(load_model(os.path.join(RES, PROJECTS[name][1])))
+    eng = get_engine(c, clf, NpScaler(os.path.join(RES, PROJECTS[name][2])), 2)
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    P = n_pop + 3
+    eng.attack_run(n_gen, P, n_off, seed, energy_ref_dirs(3, n_pop, seed=1), 0.05, 0)
+    g = torch.empty((X.shape[0], P, eng.prog.V), dtype=torch.float64, device="cuda")
+    eng.attack_population(g, None)
+    torch.cuda.synchronize()
+    return g.cpu().numpy()
+
+
+def _e2e(fixture):
+    path = os.path.join(GOLD, fixture)
+    if not os.path.exists(path):
+        pytest.skip(f"{fixture} not generated (tests/golden/make_e2e.py)")
+    d = np.load(path, allow_pickle=False)
+    name = str(d["project"])
+    B, G = int(d["n_states"]), int(d["n_gen"])
+    p = Project(name)
+    X = p.x[:B]
+    genes = _device_attack(name, X, G, int(d["n_pop"]), int(d["n_offsprings"]), int(d["seed"]))
+    sc, mn = p.ml
+    thr, eps = float(d["thr"]), float(d["eps"])
+    resp = np.zeros((B, 7), bool)
+    best = np.zeros(B)
+    same = 0
+    from make_e2e import digest
+
+    for b in range(B):
+        x_f = mo.genetic_to_ml(p.lay, genes[b], X[b])
+        obj = mo.objectives_calc(X[b], x_f, p.constraints, p.types, sc, mn, p.weights,
+                                 p.biases, 1, sc, mn, 2)
+        resp[b] = mo.objectives_respected(obj, thr, eps).any(axis=0)
+        best[b] = obj[:, 1].min()
+        same += int(digest(genes[b]) == int(d["pop_digest"][b]))
+    sr_dev, sr_ref = resp.mean(axis=0), d["success_rate"]
+    print(f"{fixture}: o1..o7 device {np.round(sr_dev, 4)} oracle {np.round(sr_ref, 4)}; "
+          f"identical final populations {same}/{B}; mean best f1 device {best.mean():.6f} "
+          f"oracle {d['best_f1'].mean():.6f}")
+    return sr_dev, sr_ref, best, d["best_f1"]
+
+
+@pytest.mark.parametrize("fixture", ["e2e_botnet_rq1.npz", "e2e_lcld_rq1_g100.npz",
+                                     "e2e_lcld_rq1_g1000.npz"])
+def test_success_rate_within_1pp_at_full_config(fixture):
+    """rq1.botnet.static: all 387 shipped states x 1000 generations (P 203, O 100, L2, eps 4,
+    thr 0.5); rq1.lcld.static: 64 synthetic states x 100 and 1000 generations (eps 0.2,
+    thr 0.25).  |o_k(device) - o_k(oracle)| <= 1 pp for every k (north_star)."""
+    import sys
+
+    sys.path.insert(0, GOLD)
+    sr_dev, sr_ref, best, best_ref = _e2e(fixture)
+    assert np.all(np.abs(sr_dev - sr_ref) <= 0.01 + 1e-12), (sr_dev, sr_ref)
+    assert abs(best.mean() - best_ref.mean()) <= 0.01

@@ -96,6 +96,115 @@ def test_predict_proba_matches_fp32_reference(name):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("name", ["botnet", "lcld", "lcld_augmented"])
+def test_evaluate_bit_exact_in_engine_order(name):
+    """mv_evaluate's F is bit-identical to the oracle's objectives restated in the engine's
+    summation orders (oracle/device_order.py): same element values, MFMA fmaf-chain order
+    for the classifier, wave-butterfly sums for f2 / f3.  (Against numpy's orders F agrees
+    to 1e-5 / 1e-12: test_evaluate_matches_reference_default_problem.)"""
+    from oracle import device_order as do
+    from moeva2_amd.problem import build_device_program, get_engine
+
+    p = Project(name)
+    c, clf, sc = make_constraints(name), make_classifier(name), make_scaler(name)
+    codes = build_device_program(c).op_code
+    eng = get_engine(c, clf, sc, 2)
+    X = p.x[:4]
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    rng = np.random.default_rng(11)
+    n = 150
+    genes = np.empty((X.shape[0], n, p.lay.V))
+    for b in range(X.shape[0]):
+        prob = p.problem(X[b])
+        gl, gu = mo.genetic_bounds(p.lay, prob.xl, prob.xu)
+        isr = np.array([t == "real" for t in mo.genetic_types(p.lay)])
+        g = np.repeat(mo.initial_population(prob, 1), n, axis=0)
+        for r in range(n):
+            k = rng.integers(0, p.lay.V, size=1 + r % 6)
+            v = rng.uniform(gl[k], gu[k])
+            g[r, k] = np.where(isr[k], v, np.round(v))
+        genes[b] = g
+    F = torch.empty((X.shape[0], n, 3), dtype=torch.float64, device="cuda")
+    eng.evaluate(torch.as_tensor(genes, device="cuda"), F)
+    F = F.cpu().numpy()
+    for b in range(X.shape[0]):
+        ref = do.evaluate_device_order(p.problem(X[b]), genes[b], codes)
+        np.testing.assert_array_equal(F[b, :, :2], ref[:, :2])
+        if name == "botnet":  # integer / ratio constraint values: identical element values
+            np.testing.assert_array_equal(F[b, :, 2], ref[:, 2])
+        else:  # LCLD's installment identity calls pow(): device pow vs numpy may differ by
+            # an ulp in a violated column (a few rows in 150)
+            np.testing.assert_allclose(F[b, :, 2], ref[:, 2], rtol=1e-14, atol=0)
+
+
+def _wide_mlp(dims=(756, 512, 512, 256, 2), seed=7):
+    """bench.py's configs[4] classifier: Dense relu x3 + softmax, weights ~ N(0, 1/fan_in)."""
+    rng = np.random.default_rng(seed)
+    W = [(rng.standard_normal((a, b)) / np.sqrt(a)).astype(np.float32)
+         for a, b in zip(dims[:-1], dims[1:])]
+    return W, [np.zeros(b, np.float32) for b in dims[1:]]
+
+
+def test_wide_mlp_config_matches_fp32_reference():
+    """BASELINE configs[4] (synthetic.botnet.wide: 756-512-512-256-2) runs the 32-row-tile
+    k_mlp path (hidden widths > 128) in the attack and k_predict in predict_proba: f1 of
+    mv_evaluate and of Classifier.predict_proba against the fp32 numpy forward (1e-5 rel),
+    f2/f3 unchanged, then a short attack keeps its invariants and is deterministic."""
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, DenseMLPModel
+    from moeva2_amd.io.tf_bundle import DenseMLP
+    from moeva2_amd.problem import get_engine
+
+    p = Project("botnet")
+    W, bs = _wide_mlp()
+    clf = Classifier(DenseMLPModel(DenseMLP(W, bs, ["relu"] * 3 + ["softmax"])))
+    c, sc = make_constraints("botnet"), make_scaler("botnet")
+    X = p.x[:6]
+    xm = X * p.ml[0] + p.ml[1]
+    ref_p = mo.mlp_predict_proba(xm, W, bs)
+    np.testing.assert_allclose(clf.predict_proba(xm), ref_p, rtol=1e-5, atol=1e-7)
+    eng = get_engine(c, clf, sc, 2)
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    rng = np.random.default_rng(5)
+    n = 37
+    genes = np.empty((X.shape[0], n, p.lay.V))
+    for b in range(X.shape[0]):
+        prob = p.problem(X[b])
+        gl, gu = mo.genetic_bounds(p.lay, prob.xl, prob.xu)
+        g = np.repeat(mo.initial_population(prob, 1), n, axis=0)
+        k = rng.integers(0, p.lay.V, size=(n, 3))
+        for r in range(n):
+            g[r, k[r]] = np.round(rng.uniform(gl[k[r]], gu[k[r]]))
+        genes[b] = g
+    gd = torch.as_tensor(genes, device="cuda")
+    F = torch.empty((X.shape[0], n, 3), dtype=torch.float64, device="cuda")
+    eng.evaluate(gd, F)
+    F = F.cpu().numpy()
+    for b in range(X.shape[0]):
+        x_f = mo.genetic_to_ml(p.lay, genes[b], X[b])
+        f1 = mo.mlp_predict_proba(x_f * p.ml[0] + p.ml[1], W, bs)[:, 1]
+        np.testing.assert_allclose(F[b, :, 0], f1, rtol=1e-5, atol=1e-7)
+        ref = mo.evaluate(p.problem(X[b]), genes[b])
+        np.testing.assert_allclose(F[b, :, 1:], ref[:, 1:], rtol=1e-12, atol=1e-15)
+    from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
+
+    ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_iter=200)
+    outs = []
+    for _ in range(2):
+        eng.attack_run(4, 23, 10, 3, ref_dirs, 0.05, 0)
+        g = torch.empty((X.shape[0], 23, p.lay.V), dtype=torch.float64, device="cuda")
+        Fa = torch.empty((X.shape[0], 23, 3), dtype=torch.float64, device="cuda")
+        eng.attack_population(g, Fa)
+        torch.cuda.synchronize()
+        outs.append((g.cpu().numpy(), Fa.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    Fe = torch.empty((X.shape[0], 23, 3), dtype=torch.float64, device="cuda")
+    eng.evaluate(torch.as_tensor(outs[0][0], device="cuda"), Fe)
+    np.testing.assert_array_equal(Fe.cpu().numpy(), outs[0][1])
+
+
 # ------------------------------------------------------------------ survival
 def _random_F(rng, B, N):
     F = np.empty((B, N, 3))
@@ -232,13 +341,18 @@ def test_tournament_selection_vs_oracle(P, O):
 
 
 # ------------------------------------------------------------------ variation
+@pytest.mark.parametrize("kind", ["two_point", "sbx"])
 @pytest.mark.parametrize("name", ["botnet", "lcld", "lcld_augmented"])
-def test_variation_vs_oracle(name):
+def test_variation_vs_oracle(name, kind):
+    """Crossover + mutation of the device (k_gen) against the oracle on identical parents and
+    Philox draws: two-point (the reference's operator, moeva2.py:90-101) and the SBX option
+    (north_star; real_sbx / int_sbx with eta 30).  Integer genes exact, real genes 1e-12."""
     from moeva2_amd.problem import get_engine
 
     p = Project(name)
     c, clf, sc = make_constraints(name), make_classifier(name), make_scaler(name)
     eng = get_engine(c, clf, sc, 2)
+    eng.set_crossover(kind, 30.0, 0.9)
     B, P, O = 3, 40, 24
     X0 = p.x[:B]
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X0]
@@ -265,22 +379,33 @@ def test_variation_vs_oracle(name):
     types = mo.genetic_types(p.lay)
     masks = [np.array([t == "real" for t in types]), np.array([t == "int" for t in types])]
     isr = masks[0]
+    eng.set_crossover("two_point")
     for b in range(B):
         pX = np.stack([pops[b][parents[:, 0]], pops[b][parents[:, 1]]])
-        ref = mo.crossover(pX, masks, 99, 5)[:O]
+        if kind == "sbx":
+            ref = mo.sbx_crossover(pX, masks, gls[b], gus[b], 99, 5, 30.0, 0.9)[:O]
+        else:
+            ref = mo.crossover(pX, masks, 99, 5)[:O]
         ref = mo.mutation(ref, gls[b], gus[b], types, 99, 5)
         np.testing.assert_array_equal(got[b][:, ~isr], ref[:, ~isr])
         np.testing.assert_allclose(got[b][:, isr], ref[:, isr], rtol=1e-12, atol=1e-12)
+    if kind == "sbx":  # the option changes the children (and keeps them in bounds)
+        cx2 = mo.crossover(np.stack([pops[0][parents[:, 0]], pops[0][parents[:, 1]]]), masks,
+                           99, 5)[:O]
+        assert not np.array_equal(got[0], mo.mutation(cx2, gls[0], gus[0], types, 99, 5))
+        assert np.all(got >= np.stack(gls)[:, None] - 1e-9) and \
+            np.all(got <= np.stack(gus)[:, None] + 1e-9)
 
 
 # ------------------------------------------------------------------ whole attack
-def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto"):
+def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto", crossover="two_point"):
     from moeva2_amd.problem import get_engine
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
     c, clf, sc = make_constraints(name), make_classifier(name), make_scaler(name)
     eng = get_engine(c, clf, sc, 2)
     eng.set_attack_mode(mode)
+    eng.set_crossover(crossover)
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
     ref = energy_ref_dirs(3, P - 3, seed=1) if P - 3 in (200, 640) else \
@@ -305,19 +430,20 @@ def mo_ref_dirs(n):
     return riesz_energy_dirs(3, n, seed=1, n_iter=200)
 
 
-@pytest.mark.parametrize("name,B,P,O,G,hist", [
-    ("botnet", 9, 203, 100, 6, 1), ("botnet_augmented", 3, 43, 20, 5, 2),
-    ("lcld", 37, 203, 100, 7, 2), ("lcld_augmented", 11, 43, 20, 6, 1),
-    ("lcld", 3, 643, 320, 3, 0)])
-def test_whole_attack_kernel_matches_phase_chain(name, B, P, O, G, hist):
+@pytest.mark.parametrize("name,B,P,O,G,hist,cx", [
+    ("botnet", 9, 203, 100, 6, 1, "two_point"), ("botnet_augmented", 3, 43, 20, 5, 2, "two_point"),
+    ("lcld", 37, 203, 100, 7, 2, "two_point"), ("lcld_augmented", 11, 43, 20, 6, 1, "two_point"),
+    ("lcld", 3, 643, 320, 3, 0, "two_point"), ("botnet", 5, 43, 20, 6, 1, "sbx"),
+    ("lcld", 9, 43, 20, 6, 2, "sbx")])
+def test_whole_attack_kernel_matches_phase_chain(name, B, P, O, G, hist, cx):
     """The one-launch attack (k_attack: one workgroup per state runs every generation) is
     bit-identical to the per-phase chain (k_gen, k_cons, k_mlp2, k_survive per generation):
     final genes, objectives and the whole history."""
     X = Project(name).x[:B]
-    e1, g1, F1, h1, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="auto")
+    e1, g1, F1, h1, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="whole", crossover=cx)
     _, whole = e1.attack_time()
     assert whole, "the shipped layout must run as one launch"
-    e2, g2, F2, h2, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="chain")
+    e2, g2, F2, h2, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="chain", crossover=cx)
     assert not e2.attack_time()[1]
     np.testing.assert_array_equal(g1.cpu().numpy(), g2.cpu().numpy())
     np.testing.assert_array_equal(F1.cpu().numpy(), F2.cpu().numpy())
@@ -426,6 +552,132 @@ def test_success_rate_matches_oracle_attack():
     sr_cpu = mo.success_rate_3d(X, x_cpu, fn, 0.25, 0.2)
     print("identical final populations:", same, "/", B, "o1..o7 dev", sr_dev, "cpu", sr_cpu)
     assert np.all(np.abs(sr_dev - sr_cpu) <= max(0.01, 1.0 / B) + 1e-12), (sr_dev, sr_cpu)
+
+
+def test_sbx_attack_matches_oracle_attack():
+    """The SBX option end to end: device attack vs the oracle's attack with sbx_crossover on
+    the same LCLD states, budget and seed (success rates within 1 pp or one state)."""
+    p = Project("lcld")
+    B, G, P, O, seed = 24, 10, 43, 20, 5
+    X = p.x[:B]
+    _, g, _, _, ref = _attack("lcld", X, G, seed, P=P, O=O, crossover="sbx")
+    genes = g.cpu().numpy()
+    sc, mn = p.ml
+
+    def fn(xi, xs):
+        return mo.objectives_calc(xi, xs, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, 2)
+
+    x_dev, x_cpu, same = [], [], 0
+    for b in range(B):
+        r = mo.run_attack(p.problem(X[b]), ref, G, P, O, seed, crossover_kind="sbx")
+        same += int(np.array_equal(r.pop_X, genes[b]))
+        x_cpu.append(mo.genetic_to_ml(p.lay, r.pop_X, X[b]))
+        x_dev.append(mo.genetic_to_ml(p.lay, genes[b], X[b]))
+    sr_dev = mo.success_rate_3d(X, x_dev, fn, 0.25, 0.2)
+    sr_cpu = mo.success_rate_3d(X, x_cpu, fn, 0.25, 0.2)
+    print("sbx identical final populations:", same, "/", B, sr_dev, sr_cpu)
+    assert np.all(np.abs(sr_dev - sr_cpu) <= max(0.01, 1.0 / B) + 1e-12), (sr_dev, sr_cpu)
+
+
+def _host_lcld_constraints():
+    """The shipped LCLD class with its device program withheld: a plugin the engine cannot
+    compile, evaluated by its own numpy ``evaluate`` (here the reference's numpy path as
+    restated by the oracle, lcld_constraints.py:168-223)."""
+    from moeva2_amd.examples.lcld.lcld_constraints import LcldConstraints
+
+    feat = os.path.join(RES, PROJECTS["lcld"][0])
+
+    class HostLcld(LcldConstraints):
+        def device_program(self):
+            raise NotImplementedError
+
+        def get_nb_constraints(self):
+            return 10
+
+        def evaluate(self, x, use_tensors=False):
+            return mo.lcld_constraints(np.atleast_2d(x))
+
+    return HostLcld(feat, feat.replace("features", "constraints"))
+
+
+class _NumpyMLP:
+    """A non-Dense-wrapper model: only predict_proba (the oracle's fp32 forward)."""
+
+    def __init__(self, name):
+        p = Project(name)
+        self.w, self.b = p.weights, p.biases
+
+    def predict_proba(self, x):
+        return mo.mlp_predict_proba(np.asarray(x, np.float64), self.w, self.b)
+
+
+def test_hosted_constraints_plugin_default_problem():
+    """A Constraints subclass without a device program goes through its own evaluate on the
+    host: DefaultProblem._evaluate F equals the device program's F (f3 to
+    1e-12; f1, f2 identical) and the full history carries the host G."""
+    from moeva2_amd.attacks.moeva2.default_problem import DefaultProblem
+    from moeva2_amd.attacks.moeva2.feature_encoder import get_encoder_from_constraints
+
+    p = Project("lcld")
+    x0 = p.x[3]
+    ch, cd = _host_lcld_constraints(), make_constraints("lcld")
+    clf, sc = make_classifier("lcld"), make_scaler("lcld")
+    rng = np.random.default_rng(1)
+    prob = p.problem(x0)
+    gl, gu = mo.genetic_bounds(p.lay, prob.xl, prob.xu)
+    g = np.repeat(mo.initial_population(prob, 1), 30, axis=0)
+    k = rng.integers(0, p.lay.V, size=30)
+    g[np.arange(30), k] = np.round(rng.uniform(gl[k], gu[k]))
+    outs = []
+    for c in (ch, cd):
+        pr = DefaultProblem(x0, clf, 1, get_encoder_from_constraints(c, x0), c, True,
+                            save_history="full", ml_scaler=sc, norm=2)
+        out = {}
+        pr._evaluate(g, out)
+        outs.append((out["F"], pr.get_history()[0]))
+    np.testing.assert_array_equal(outs[0][0][:, :2], outs[1][0][:, :2])
+    np.testing.assert_allclose(outs[0][0][:, 2], outs[1][0][:, 2], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("which", ["constraints", "classifier"])
+def test_hosted_plugins_attack(which):
+    """Moeva2.generate with a host plugin (constraints without a device program, or a model
+    with only predict_proba) runs the host-driven loop around the device calls: it tracks
+    the all-device attack (same draws; only the host columns' rounding differs) and its
+    final objectives are the plugin's own values."""
+    from moeva2_amd.attacks.moeva2.classifier import Classifier
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+
+    p = Project("lcld")
+    B, G = 8, 4
+    X = p.x[:B]
+    model = os.path.join(RES, PROJECTS["lcld"][1])
+    host = Moeva2(model, _host_lcld_constraints() if which == "constraints"
+                  else make_constraints("lcld"), ml_scaler=make_scaler("lcld"), norm=2,
+                  n_gen=G, n_pop=200, n_offsprings=100, seed=4)
+    if which == "classifier":
+        host._classifier = Classifier(_NumpyMLP("lcld"))
+    dev = Moeva2(model, make_constraints("lcld"), ml_scaler=make_scaler("lcld"), norm=2,
+                 n_gen=G, n_pop=200, n_offsprings=100, seed=4)
+    gh, Fh, _ = host.generate(X, 1, return_device=True)
+    gd, Fd, _ = dev.generate(X, 1, return_device=True)
+    gh, Fh, gd, Fd = (t.cpu().numpy() for t in (gh, Fh, gd, Fd))
+    same = [b for b in range(B) if np.array_equal(gh[b], gd[b])]
+    print(which, "identical final populations", len(same), "/", B)
+    assert len(same) >= B // 2
+    for b in same:
+        np.testing.assert_allclose(Fh[b], Fd[b], rtol=1e-5, atol=1e-12)
+    for b in range(B):  # host columns are the plugin's values on the final population
+        x_f = mo.genetic_to_ml(p.lay, gh[b], X[b])
+        if which == "constraints":
+            gg = mo.lcld_constraints(x_f)
+            np.testing.assert_array_equal(Fh[b, :, 2], (gg * (gg > 0)).sum(1))
+        else:
+            sc, mn = p.ml
+            f1 = mo.mlp_predict_proba(x_f * sc + mn, p.weights, p.biases)[:, 1]
+            np.testing.assert_array_equal(Fh[b, :, 0], f1.astype(np.float64))
 
 
 def _objcalc(name, norm=2, thr=(0.5, 4), ml=True):

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--workload", default="rq1.botnet.static")
     ap.add_argument("--n-gen", type=int, default=None)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--modes", default="auto,chain")
+    ap.add_argument("--modes", default="whole,chain")
     args = ap.parse_args()
     import torch
 
