@@ -9,11 +9,15 @@ step   : one full MoEvA2 attack (all states, n_gen generations: init + evaluate,
 workload (N=1): configs[1] = rq1.botnet.static -- the 387 shipped CTU-13 botnet states,
          n_pop 200 (P = 203), n_offsprings 100, budget 1000 generations, L2, history
          "reduced" (config/moeva.yaml, config/rq1.botnet.static.yaml, config/rq1.botnet.yaml).
-multi-GPU: states are independent (moeva2.py:194-205): every rank runs the same per-GPU
-         workload on its own seed (weak scaling), no collective inside the attack; one
-         all_gather of the per-state best misclassification value closes the step.
+multi-GPU: states are independent (moeva2.py:194-205).  Default (weak scaling): every rank
+         attacks the workload's full state set with its own seed (seed 42 + rank: N
+         independent attack replicas), no collective inside the attack; one all_gather of
+         the per-state best misclassification value closes the step.  --shard (strong
+         scaling): the states are split over the ranks (moeva2_amd.distributed.shard_bounds,
+         as Moeva2.generate_sharded), each rank attacks its slice, one all_gather.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--shard]
+                    [--mode auto|chain|whole] [--crossover two_point|sbx]
 """
 import argparse
 import json
@@ -121,30 +125,69 @@ def build_engine(w, device):
     return eng, c
 
 
-def cpu_baseline(w, sample_states=1, sample_gens=100):
-    """Oracle ("port") CPU statement of the same loop, 1 core, bounded sample."""
+_CPU_PROJECT = None
+
+
+def _cpu_init(project):
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from threadpoolctl import threadpool_limits
+
+    threadpool_limits(1)  # one core per process: the numpy MLP's BLAS stays single-threaded
     sys.path.insert(0, ROOT)
-    from oracle import moeva_oracle as mo
+    sys.path.insert(0, PKG)
+    global _CPU_PROJECT
     from oracle.problems import Project
+
+    _CPU_PROJECT = Project(project)
+
+
+def _cpu_noop(_):
+    return os.getpid()
+
+
+def _cpu_state(args):
+    s, n_pop, n_off, gens, norm, history = args
+    from oracle import moeva_oracle as mo
 
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
-    from threadpoolctl import threadpool_limits
+    p = _CPU_PROJECT
+    ref = energy_ref_dirs(3, n_pop, seed=1)
+    mo.run_attack(p.problem(p.x[s % p.x.shape[0]], norm=norm), ref, gens, n_pop + 3, n_off,
+                  seed=42, save_history=history)
+    return n_pop + 3 + (gens - 1) * n_off
 
-    p = Project(w["project"])
-    ref = energy_ref_dirs(3, w["n_pop"], seed=1)
+
+def cpu_cores():
+    """Host cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box; os.cpu_count() there reports the whole machine), else os.cpu_count()."""
+    n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n
+
+
+def cpu_baseline(w, sample_gens=100, cores=None):
+    """The oracle's CPU statement of the same loop (eval + survival + variation, numpy):
+    one process per host core, one initial state per process (like the reference's
+    joblib pool over states, n_jobs = cores), a bounded sample of generations."""
+    from multiprocessing import get_context
+
+    cores = cores or cpu_cores()
     P, O = w["n_pop"] + 3, w["n_off"]
-    n_eval = 0
-    with threadpool_limits(limits=1):  # one core: BLAS in the numpy MLP stays single-threaded
+    jobs = [(s, w["n_pop"], w["n_off"], sample_gens, w["norm"], w["history"])
+            for s in range(cores)]
+    with get_context("spawn").Pool(cores, initializer=_cpu_init,
+                                   initargs=(w["project"],)) as pool:
+        pool.map(_cpu_noop, range(4 * cores))  # every worker started and initialised
         t0 = time.perf_counter()
-        for s in range(sample_states):
-            mo.run_attack(p.problem(p.x[s], norm=w["norm"]), ref, sample_gens, P, O, seed=42,
-                          save_history=w["history"])
-            n_eval += P + (sample_gens - 1) * O
+        n_eval = sum(pool.map(_cpu_state, jobs, chunksize=1))
         dt = time.perf_counter() - t0
-    return {"value": n_eval / dt, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_states} {w['project']} state(s) x {sample_gens} generations "
-                      f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack, numpy, 1 process",
+    return {"value": n_eval / dt, "unit": "evals/s", "cores": cores, "kind": "port",
+            "sample": f"{cores} {w['project']} states x {sample_gens} generations "
+                      f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack (numpy), one "
+                      f"process per core, os.cpu_count()={os.cpu_count()}",
             "seconds": dt}
 
 
@@ -171,8 +214,12 @@ def main():
                     help="state groups (streams) of the timed attack; default: engine's choice. "
                          "--groups 1 makes every launch cover all states, like the roofline "
                          "pass, so rocprofv3 averages compare 1:1 with the bench's event times")
+    ap.add_argument("--mode", default="auto", choices=["auto", "chain", "whole"],
+                    help="attack schedule: per-phase kernel chain or one whole-attack launch")
+    ap.add_argument("--crossover", default="two_point", choices=["two_point", "sbx"])
+    ap.add_argument("--shard", action="store_true",
+                    help="strong scaling: split the states over the ranks")
     ap.add_argument("--cpu-gens", type=int, default=300)
-    ap.add_argument("--cpu-states", type=int, default=2)
     args = ap.parse_args()
 
     if args.groups:
@@ -193,11 +240,19 @@ def main():
         w["n_gen"] = args.n_gen
     from moeva2_amd.attacks.moeva2.moeva2 import history_mode
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+    from moeva2_amd.distributed import all_gather_states, shard_bounds
 
     t_load = time.perf_counter()
     eng, c = build_engine(w, device)
-    X = load_states(w)
+    eng.set_attack_mode(args.mode)
+    eng.set_crossover(args.crossover)
+    X_all = load_states(w)
+    B_all = X_all.shape[0]
+    lo, hi = shard_bounds(B_all, world, rank) if args.shard else (0, B_all)
+    X = X_all[lo:hi]
     B = X.shape[0]
+    if B == 0:
+        raise SystemExit(f"rank {rank}: no states in its shard ({B_all} states, {world} ranks)")
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
     ref = energy_ref_dirs(3, w["n_pop"], seed=1)
@@ -209,13 +264,17 @@ def main():
     gathered = torch.empty((world, B), dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
-    seed = 42 + rank
+    # weak: every rank attacks the whole state set, rank r with seed 42 + r (replicas);
+    # strong (--shard): one seed, the states split over the ranks (generate_sharded)
+    seed = 42 if args.shard else 42 + rank
 
     def step():
         eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
         eng.attack_population(genes, F)
         best = F[:, :, 0].min(dim=1).values.contiguous()
-        if world > 1:
+        if world > 1 and args.shard:
+            all_gather_states(best, B_all)
+        elif world > 1:
             dist.all_gather_into_tensor(gathered, best)
         else:
             gathered[0].copy_(best)
@@ -241,42 +300,48 @@ def main():
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed:.3f}s")
 
     evals_per_state = P + (G - 1) * O
-    total_evals = world * B * evals_per_state * args.steps
+    states_total = B_all if args.shard else world * B_all
+    total_evals = states_total * evals_per_state * args.steps
     value = total_evals / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # ---- roofline of the dominant kernels, measured live with HIP events that the engine
-    # records on the bench stream around every k_vary / k_mlp / k_survive launch
+    # ---- roofline of the dominant kernel, measured live with HIP events that the engine
+    # records on the bench stream around every launch (one state group, so each launch
+    # covers all states of the rank like the rocprofv3 pass of the same command)
     eng.set_profiling(True)
     eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
+    att_ms, whole = eng.attack_time()
     eng.set_profiling(False)
-    ng = max(kt["generations"], 1)
-    gen_ms = kt["gen_ms"] / ng
-    cons_ms = kt["cons_ms"] / ng
-    mlp_ms = kt["mlp_ms"] / ng
-    surv_ms = kt["survive_ms"] / ng
     rows = B * O
     Dm = int(eng.prog.mut_feats.shape[0])
-    Dm4 = (Dm + 3) // 4 * 4
-    # algorithmic bytes per offspring row (SURVEY.md §8d form):
+    Dm4 = (Dm + 15) // 16 * 16
+    # algorithmic work per candidate evaluation: bytes = 2*V*8 (offspring
+    # genes written + read once as parents) + 3*8 (F); FLOPs = 2*sum(in*out) over the full
+    # Dense chain (dims[0] = D).  The engine executes fewer FLOPs: the immutable features of
+    # layer 1 are folded into a per-state bias (executed_flops below).
+    eval_bytes = 2 * V * 8 + 3 * 8
+    dims_full = list(eng_dims(eng))
+    eval_flops = 2 * sum(a * b for a, b in zip(dims_full[:-1], dims_full[1:]))
+    dims_exec = [Dm] + dims_full[1:]
+    exec_flops = 2 * sum(a * b for a, b in zip(dims_exec[:-1], dims_exec[1:]))
+    # per-kernel algorithmic bytes per offspring row:
     #   k_gen : parent genes read + child genes written (2*V*8) + fp32 ML row (Dm4*4) + f2 (8)
     #   k_cons: child genes read (V*8) + f3 (8)
     #   k_survive: merged F read (N*3*8) + survivor/free slots + parents (4*(P+O+O)) per state
     gen_bytes = 2 * V * 8 + Dm4 * 4 + 8
     cons_bytes = V * 8 + 8
     surv_bytes_state = (P + O) * 3 * 8 + 4 * (P + 2 * O)
-    dims = [Dm] + list(eng_dims(eng))[1:]
-    mlp_flops = 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
 
-    # HBM bytes per launch from the committed rocprofv3 PMC passes of this workload
-    # (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 FETCH correction)
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of THIS workload and
+    # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if w["project"] == "botnet" and os.path.exists(tpath):
+    tpath = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{args.workload}_{args.mode}.json")
+    if os.path.exists(tpath) and args.crossover == "two_point":
         with open(tpath) as fh:
-            traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()}
+            traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()
+                       if isinstance(v, dict) and "traffic_bytes" in v}
 
     def hbm(name, bytes_launch, ms, key):
         gbs = bytes_launch / (ms * 1e-3) / 1e9
@@ -284,20 +349,41 @@ def main():
                 "frac": gbs / HBM_PEAK_GBS, "traffic": traffic.get(key), "kernel": name,
                 "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": ms}
 
-    kernels = {
-        "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows, gen_ms,
-                     "k_gen"),
-        "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
-                      "k_cons"),
-        "k_mlp": {"bound": "mfma", "achieved": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12,
-                  "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                  "frac": mlp_flops * rows / (mlp_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
-                  "traffic": traffic.get("k_mlp"), "kernel": "k_mlp (fp32 MFMA Dense chain)",
-                  "algorithmic_flops_per_launch": mlp_flops * rows, "avg_launch_ms": mlp_ms},
-        "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
-                         surv_bytes_state * B, surv_ms, "k_survive"),
-    }
-    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+    if whole:
+        n_launch_evals = B * evals_per_state
+        kernels = {"k_attack": hbm("k_attack (whole attack: one launch, one workgroup per "
+                                   "state)", eval_bytes * n_launch_evals, att_ms, "k_attack")}
+        kernels["k_attack"]["mfma_tflops"] = eval_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
+        per_gen = {"k_attack_ms_per_attack": att_ms, "dominant": "k_attack"}
+    else:
+        ng = max(kt["generations"], 1)
+        gen_ms = kt["gen_ms"] / ng
+        cons_ms = kt["cons_ms"] / ng
+        mlp_ms = kt["mlp_ms"] / ng
+        surv_ms = kt["survive_ms"] / ng
+        mlp_tfs = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
+        kernels = {
+            "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows,
+                         gen_ms, "k_gen"),
+            "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
+                          "k_cons"),
+            "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": MFMA_F32_PEAK_TFS,
+                      "unit": "TFLOP/s", "frac": mlp_tfs / MFMA_F32_PEAK_TFS,
+                      "traffic": traffic.get("k_mlp"), "kernel": "k_mlp (fp32 MFMA Dense chain)",
+                      "algorithmic_flops_per_launch": eval_flops * rows,
+                      "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},
+            "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
+                             surv_bytes_state * B, surv_ms, "k_survive"),
+        }
+        per_gen = {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+        per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+    dom = per_gen["dominant"]
+    if args.shard:
+        par = (f"states sharded over {world} rank(s): {B} of {B_all} on rank {rank}; one "
+               "all_gather of per-state results")
+    else:
+        par = (f"{world} rank(s), each attacking all {B_all} states with its own seed "
+               "(independent replicas); one all_gather of per-state results")
 
     result = {
         "metric": "candidate fitness evals/sec (whole node) + attack wall-clock per 1k states",
@@ -308,24 +394,27 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": data_note(w, B),
-        "config": {"workload": args.workload, "states_per_gpu": B, "pop_size": P,
-                   "n_offsprings": O, "n_gen": G, "norm": w["norm"], "history": w["history"],
-                   "evals_per_state": evals_per_state, "classifier_dtype": "f32 (MFMA)",
-                   "parallelism": f"states x{world} (independent per-rank shards)"},
-        "attack_wall_clock_per_1k_states_s": elapsed / args.steps / (world * B) * 1000.0,
+        "data": data_note(w, B_all),
+        "config": {"workload": args.workload, "states": B_all, "states_per_gpu": B,
+                   "pop_size": P, "n_offsprings": O, "n_gen": G, "norm": w["norm"],
+                   "history": w["history"], "evals_per_state": evals_per_state,
+                   "classifier_dtype": "f32 (MFMA)", "crossover": args.crossover,
+                   "schedule": "whole-attack kernel" if whole else "per-phase kernel chain",
+                   "parallelism": par},
+        "attack_wall_clock_per_1k_states_s": elapsed / args.steps / states_total * 1000.0,
         "load_s": load_s,
         "roofline": kernels[dom],
         "kernels": kernels,
-        "kernels_avg_ms_per_generation": {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms,
-                                          "k_survive": surv_ms, "dominant": dom},
+        "kernels_avg_ms_per_generation": per_gen,
+        "algorithmic_per_eval": {"bytes": eval_bytes, "flops": eval_flops,
+                                 "executed_flops": exec_flops},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1 and \
             not w["model"].startswith("synthetic:"):
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_states, args.cpu_gens)
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_gens)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

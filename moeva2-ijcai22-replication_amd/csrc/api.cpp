@@ -898,8 +898,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       hipStream_t st = gs[q];
       const bool prof = e->profiling && q == 0;
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
-      HIPCHK(launch_vary(vq[q], slot_va[q], g, hist_row0, st));  // k_rows (or k_gen + k_cons)
+      HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+      HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
       HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));

@@ -88,29 +88,34 @@ __device__ __forceinline__ void mlp_state(const RowsArgs& a, const int b, const 
   constexpr int U = 1024 / T;  // float4 per thread per 64 x 64 chunk
   for (int tile = 0; tile < ntiles; ++tile) {
     const int r0 = tile * M2_ROWS;
-    float4 st[U];
-    auto chunk_load = [&](int c) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int idx = tid + T * u;
-        const int row = idx >> 4, q = idx & 15;
-        const int k = c * 64 + 4 * q < K0 ? c * 64 + 4 * q : K0 - 4;
-        const int rr = r0 + row < n ? r0 + row : n - 1;
-        st[u] = *(const float4*)(a.xml + (rbase + rr) * K0 + k);
-      }
-    };
-    auto chunk_store = [&](int buf) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int idx = tid + T * u;
-        const int row = idx >> 4, q = idx & 15;
-        *(float4*)(A0 + buf * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = st[u];
-      }
-    };
-    chunk_load(0);
+    // staging registers as plain locals (a lambda-captured array is address-taken -> scratch)
+    float4 st0, st1, st2, st3;
+    static_assert(U <= 4, "chunk staging holds at most 4 float4 per thread");
+#define MS_CHUNK_LOAD(c)                                                                 \
+  {                                                                                      \
+    const int cc = (c);                                                                  \
+    float4* sts[4] = {&st0, &st1, &st2, &st3};                                           \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                      \
+      const int idx = tid + T * u;                                                       \
+      const int row = idx >> 4, q = idx & 15;                                            \
+      const int k = cc * 64 + 4 * q < K0 ? cc * 64 + 4 * q : K0 - 4;                     \
+      const int rr = r0 + row < n ? r0 + row : n - 1;                                    \
+      *sts[u] = *(const float4*)(a.xml + (rbase + rr) * K0 + k);                         \
+    }                                                                                    \
+  }
+#define MS_CHUNK_STORE(buf)                                                              \
+  {                                                                                      \
+    const float4 vs[4] = {st0, st1, st2, st3};                                           \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                      \
+      const int idx = tid + T * u;                                                       \
+      const int row = idx >> 4, q = idx & 15;                                            \
+      *(float4*)(A0 + (buf) * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = vs[u];           \
+    }                                                                                    \
+  }
+    MS_CHUNK_LOAD(0)
     __syncthreads();  // the previous tile's (or phase's) readers of the LDS are done
     if (tid < M2_ROWS) rowst[tid] = r0 + tid < n ? b : -1;
-    chunk_store(0);
+    MS_CHUNK_STORE(0)
     __syncthreads();
     floatx4 acc[CJ][4];
 #pragma unroll
@@ -119,14 +124,16 @@ __device__ __forceinline__ void mlp_state(const RowsArgs& a, const int b, const 
       for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
     const TileMap m0 = tile_map_w(N0 >> 4, wave, W);
     for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) chunk_load(c + 1);
+      if (c + 1 < nch) MS_CHUNK_LOAD(c + 1)
       const int ng = min(4, nkg0 - 4 * c);
       if (m0.nrt > 0)
         mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
                        p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, m0, il, ka);
-      if (c + 1 < nch) chunk_store((c + 1) & 1);
+      if (c + 1 < nch) MS_CHUNK_STORE((c + 1) & 1)
       __syncthreads();
     }
+#undef MS_CHUNK_LOAD
+#undef MS_CHUNK_STORE
     for (int l = 0; l + 1 < nl; ++l) {
       const int N = p.dims[l + 1];
       const TileMap m = tile_map_w(N >> 4, wave, W);
@@ -189,11 +196,15 @@ __device__ __forceinline__ void mlp_state(const RowsArgs& a, const int b, const 
     if (tid < M2_ROWS && r0 + tid < n) {
       double z[8];
       double mx = -__builtin_inf();
-      for (int c = 0; c < nout; ++c) {
-        const float* q = part + tid * nout + c;
-        z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
-                         q[3 * M2_ROWS * nout]) + bl[c]);
-        mx = z[c] > mx ? z[c] : mx;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        z[c] = 0.0;
+        if (c < nout) {
+          const float* q = part + tid * nout + c;
+          z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
+                           q[3 * M2_ROWS * nout]) + bl[c]);
+          mx = z[c] > mx ? z[c] : mx;
+        }
       }
       const double f1 = softmax_pick(z, nout, mx, a.s.min_class[b]);
       const int i = r0 + tid;

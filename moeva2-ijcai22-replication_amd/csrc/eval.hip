@@ -90,7 +90,9 @@ hipError_t release_rows(int slot, hipStream_t stream) {
 // mutations are precomputed for all of a wave's rows at once, one row per lane: mutations
 // are a geometric-gap process (about two Philox draws per row instead of one word per
 // gene), at most MUT_CAP per row cached in registers, the rare rest finished in the row.
-template <bool IDENT, int NT>
+// SBX: the SBX crossover option compiled in (a separate instance: its pow()-heavy path
+// doubled the two-point kernel's registers, halving its occupancy).
+template <bool IDENT, int NT, bool SBX>
 __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
   const Rng rng(a.seed, a.stream_key);
   const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
   const double* sgu = a.s.gu + (size_t)b * V;
-  const bool sbx = a.mode == 1 && a.cx_kind == 1;
+  const bool sbx = SBX && a.mode == 1;
   const bool mine = lane < nrw;
   const int irow = rc.i0 + wave + 4 * lane;
   if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
@@ -583,15 +585,18 @@ __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi
 // fp32 logits, softmax in fp64 rounded to fp32 (softmax_pick).
 __device__ __forceinline__ void last_layer_softmax(const float* in, int ldi, int K, int nout,
                                                    const float* ws, const float* wsb, int t,
-                                                   float* prob) {
+                                                   float (&prob)[8]) {
   double z[8];
   double mx = -__builtin_inf();
-  for (int c = 0; c < nout; ++c) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], ws[k * nout + c], s);
-    z[c] = (double)(s + wsb[c]);
-    mx = z[c] > mx ? z[c] : mx;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    z[c] = 0.0;
+    if (c < nout) {
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s = fmaf(in[t * ldi + k], ws[k * nout + c], s);
+      z[c] = (double)(s + wsb[c]);
+      mx = z[c] > mx ? z[c] : mx;
+    }
   }
   softmax_all(z, nout, mx, prob);
 }
@@ -709,31 +714,35 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
   const int nch = (nkg0 + 3) >> 2;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int r0 = tile * M2_ROWS;
-    float4 st[4];
-    auto chunk_load = [&](int c) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int idx = tid + 256 * u;
-        const int row = idx >> 4, q = idx & 15;
-        // clamped, unconditional loads: rows past the end are computed but never written,
-        // k past K0 is never multiplied (the last chunk runs only its nkg0 % 4 groups)
-        const int k = c * 64 + 4 * q < K0 ? c * 64 + 4 * q : K0 - 4;
-        const int rr = r0 + row < a.total ? r0 + row : a.total - 1;
-        st[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);
-      }
-    };
-    auto chunk_store = [&](int buf) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int idx = tid + 256 * u;
-        const int row = idx >> 4, q = idx & 15;
-        *(float4*)(A0 + buf * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = st[u];
-      }
-    };
-    chunk_load(0);
+    // the chunk staging registers are plain locals: captured by a lambda they were
+    // address-taken and lived in scratch (64 B per lane per chunk, 41 MiB of WRITE_SIZE per
+    // launch in the r01 PMC pass)
+    float4 st0, st1, st2, st3;
+#define M2_CHUNK_LOAD(c)                                                                 \
+  {                                                                                      \
+    const int cc = (c);                                                                  \
+    float4* sts[4] = {&st0, &st1, &st2, &st3};                                           \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                      \
+      const int idx = tid + 256 * u;                                                     \
+      const int row = idx >> 4, q = idx & 15;                                            \
+      const int k = cc * 64 + 4 * q < K0 ? cc * 64 + 4 * q : K0 - 4;                     \
+      const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                        \
+      *sts[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);                           \
+    }                                                                                    \
+  }
+#define M2_CHUNK_STORE(buf)                                                              \
+  {                                                                                      \
+    const float4 vs[4] = {st0, st1, st2, st3};                                           \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                      \
+      const int idx = tid + 256 * u;                                                     \
+      const int row = idx >> 4, q = idx & 15;                                            \
+      *(float4*)(A0 + (buf) * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = vs[u];           \
+    }                                                                                    \
+  }
+    M2_CHUNK_LOAD(0)
     __syncthreads();  // the previous tile's readers of rowst / A0 / H are done
     if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
-    chunk_store(0);
+    M2_CHUNK_STORE(0)
     __syncthreads();
     floatx4 acc[CJ][4];
 #pragma unroll
@@ -741,13 +750,15 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) chunk_load(c + 1);
+      if (c + 1 < nch) M2_CHUNK_LOAD(c + 1)
       const int ng = min(4, nkg0 - 4 * c);
       mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, p.Wp[0] + (size_t)4 * c * N0 * 16,
                      ng, N0, acc, tile_map(N0 >> 4, wave), il, ka);
-      if (c + 1 < nch) chunk_store((c + 1) & 1);
+      if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1)
       __syncthreads();
     }
+#undef M2_CHUNK_LOAD
+#undef M2_CHUNK_STORE
     // hidden layers: layer l writes H[l & 1]
     for (int l = 0; l + 1 < nl; ++l) {
       const int N = p.dims[l + 1];
@@ -820,11 +831,15 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
       if (s >= 0) {
         double z[8];
         double mx = -__builtin_inf();
-        for (int c = 0; c < nout; ++c) {
-          const float* q = part + tid * nout + c;
-          z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
-                           q[3 * M2_ROWS * nout]) + bl[c]);
-          mx = z[c] > mx ? z[c] : mx;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          z[c] = 0.0;
+          if (c < nout) {
+            const float* q = part + tid * nout + c;
+            z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
+                             q[3 * M2_ROWS * nout]) + bl[c]);
+            mx = z[c] > mx ? z[c] : mx;
+          }
         }
         const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
         const int i = r0 + tid - s * a.n;
@@ -1063,13 +1078,18 @@ static int vary_nt(const DProblem& p) {
 }
 
 template <bool IDENT, int NT>
-static hipError_t gen_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw) {
+static hipError_t gen_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw,
+                         bool sbx) {
   static bool configured = false;
   if (!configured) {
-    allow_lds(k_gen<IDENT, NT>);
+    allow_lds(k_gen<IDENT, NT, false>);
+    allow_lds(k_gen<IDENT, NT, true>);
     configured = true;
   }
-  hipLaunchKernelGGL((k_gen<IDENT, NT>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  if (sbx)
+    hipLaunchKernelGGL((k_gen<IDENT, NT, true>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  else
+    hipLaunchKernelGGL((k_gen<IDENT, NT, false>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
   return hipGetLastError();
 }
 
@@ -1092,7 +1112,8 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
   const int nt = vary_nt(a.p);
   const bool ident = a.p.ident != 0;
   const size_t lds = gen_lds(vary_offsets(a.p), gen_regc(a.p, nt), ident, a.do_eval != 0).total;
-#define GEN(I, N) return gen_go<I, N>(grid, lds, stream, slot, gen, hist_row0, rw)
+  const bool sbx = a.mode == 1 && a.cx_kind == 1;
+#define GEN(I, N) return gen_go<I, N>(grid, lds, stream, slot, gen, hist_row0, rw, sbx)
   if (ident) {
     if (nt == 1) GEN(true, 1);
     if (nt == 2) GEN(true, 2);

@@ -421,22 +421,32 @@ __device__ __forceinline__ double rdl_d(double v, int k) {
 // final rounding make the value a function of the logits alone -- independent of the expf
 // implementation -- so a CPU restatement reproduces it bit for bit
 // (oracle/device_order.py); it is within an fp32 ulp of Keras' fp32 softmax.
-// z is overwritten with the exponentials; softmax_all writes every class's probability.
-__device__ __forceinline__ double softmax_pick(double* z, int nout, double mx, int c) {
-  double den = 0.0;
-  for (int k = 0; k < nout; ++k) {
-    z[k] = exp(z[k] - mx);
-    den = den + z[k];
+// Fully unrolled over the at most 8 classes (a runtime-indexed array would live in scratch).
+__device__ __forceinline__ double softmax_pick(const double (&z)[8], int nout, double mx, int c) {
+  double den = 0.0, pc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (k < nout) {
+      const double e = exp(z[k] - mx);
+      den = den + e;
+      pc = k == c ? e : pc;
+    }
   }
-  return (double)(float)(z[c] / den);
+  return (double)(float)(pc / den);
 }
-__device__ __forceinline__ void softmax_all(double* z, int nout, double mx, float* prob) {
-  double den = 0.0;
-  for (int k = 0; k < nout; ++k) {
-    z[k] = exp(z[k] - mx);
-    den = den + z[k];
+__device__ __forceinline__ void softmax_all(const double (&z)[8], int nout, double mx,
+                                            float (&prob)[8]) {
+  double e[8], den = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    e[k] = 0.0;
+    if (k < nout) {
+      e[k] = exp(z[k] - mx);
+      den = den + e[k];
+    }
   }
-  for (int k = 0; k < nout; ++k) prob[k] = (float)(z[k] / den);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) prob[k] = (float)(e[k] / den);
 }
 
 // Async global -> LDS copy of nbytes (a 1-KiB multiple): 16 B per lane, 1 KiB per wave
