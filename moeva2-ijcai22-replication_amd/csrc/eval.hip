@@ -26,6 +26,7 @@
 
 #include "engine.h"
 #include "kernels.h"
+#include "narrow.h"
 #include "philox.h"
 #include "rowops.h"
 #include "rows_fused.h"
@@ -504,6 +505,13 @@ __global__ __launch_bounds__(VARY_T) void k_rows(int slot, int gen, int hist_row
   const int b = id / nchunk;
   const int r0 = (id - b * nchunk) * rows_wg;
   rows_state<IDENT, NT, FULL, VARY_T>(a, b, gen, hist_row0, r0, min(a.n, r0 + rows_wg), smem);
+}
+
+// k_narrow: k_gen + k_cons for narrow rows, one lane per row (narrow.h).
+template <int NV, bool FULL>
+__global__ __launch_bounds__(NARROW_T) void k_narrow(int slot, int gen, int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  narrow_rows<NV, FULL>(c_rows[slot], gen, hist_row0, smem);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1104,8 +1112,43 @@ static hipError_t cons_go(dim3 grid, size_t lds, hipStream_t s, int slot, int h0
   return hipGetLastError();
 }
 
+// Narrow rows (LCLD-shaped problems): k_narrow does k_gen's and k_cons's work in one launch
+// (two-point crossover; the SBX option and variation-only launches keep the wave-per-row
+// kernels).  MV_NARROW=0 turns it off (A/B runs).
+static bool use_narrow(const RowsArgs& a) {
+  const char* s = std::getenv("MV_NARROW");  // read per launch: tests flip it in-process
+  return !(s && s[0] == '0') && a.do_eval && narrow_ok(a.p) && !(a.mode == 1 && a.cx_kind == 1);
+}
+
+template <int NV, bool FULL>
+static hipError_t narrow_go(const RowsArgs& a, int slot, int gen, int hist_row0,
+                            hipStream_t stream) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_narrow<NV, FULL>);
+    configured = true;
+  }
+  const size_t lds = narrow_lds(vary_offsets(a.p), a.p).total;
+  const dim3 grid((unsigned)((a.total + NARROW_T - 1) / NARROW_T));
+  hipLaunchKernelGGL((k_narrow<NV, FULL>), grid, dim3(NARROW_T), lds, stream, slot, gen,
+                     hist_row0);
+  return hipGetLastError();
+}
+
+static hipError_t launch_narrow(const RowsArgs& a, int slot, int gen, int hist_row0,
+                                hipStream_t stream) {
+#define NG(NV) \
+  return a.p.full_ops ? narrow_go<NV, true>(a, slot, gen, hist_row0, stream) \
+                      : narrow_go<NV, false>(a, slot, gen, hist_row0, stream)
+  if (a.p.V <= 8) NG(8);
+  if (a.p.V <= 16) NG(16);
+  NG(32);
+#undef NG
+}
+
 hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
+  if (use_narrow(a)) return launch_narrow(a, slot, gen, hist_row0, stream);
   const int B = a.total / a.n;
   const int rw = vary_rows_per_wg(a.n);
   const dim3 grid(B * ((a.n + rw - 1) / rw));
@@ -1131,6 +1174,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
 
 hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || !a.do_eval) return hipSuccess;
+  if (use_narrow(a)) return hipSuccess;  // done by k_narrow in launch_gen
   const int B = a.total / a.n;
   const int rw = vary_rows_per_wg(a.n);
   const dim3 grid(B * ((a.n + rw - 1) / rw));

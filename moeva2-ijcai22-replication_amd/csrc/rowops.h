@@ -52,8 +52,10 @@ __device__ __forceinline__ OpTab global_tab(const DProblem& p) {
 
 // One constraint column on the ML row x (LDS).  FULL adds the LCLD financial identities;
 // ABS_SUMDIFF columns are evaluated wave-parallel (sumdiff_wave) by the caller.
-template <bool FULL>
-__device__ __forceinline__ double eval_op(const OpTab& t, int c, const double* __restrict__ x) {
+// XR: the row accessor -- a pointer to the LDS row, or any type with operator[](int) (the
+// narrow-row kernel's lane-strided row, narrow.h).
+template <bool FULL, class XR>
+__device__ __forceinline__ double eval_op(const OpTab& t, int c, const XR& x) {
   const int code = t.code[c];
   const int4 ar = t.arg[c];
   switch (code) {
