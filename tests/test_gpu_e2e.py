@@ -80,9 +80,10 @@ def _e2e(fixture):
         best[b] = obj[:, 1].min()
         same += int(digest(genes[b]) == int(d["pop_digest"][b]))
     sr_dev, sr_ref = resp.mean(axis=0), d["success_rate"]
+    same_f1 = int((best == d["best_f1"]).sum())
     print(f"{fixture}: o1..o7 device {np.round(sr_dev, 4)} oracle {np.round(sr_ref, 4)}; "
-          f"identical final populations {same}/{B}; mean best f1 device {best.mean():.6f} "
-          f"oracle {d['best_f1'].mean():.6f}")
+          f"identical final populations {same}/{B}; identical best f1 {same_f1}/{B}; mean best "
+          f"f1 device {best.mean():.6f} oracle {d['best_f1'].mean():.6f}")
     return sr_dev, sr_ref, best, d["best_f1"]
 
 
