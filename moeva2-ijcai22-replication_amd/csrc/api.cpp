@@ -36,7 +36,13 @@ template <class T>
 hipError_t dalloc(T** p, size_t n) {
   *p = nullptr;
   if (n == 0) n = 1;
-  return hipMalloc((void**)p, n * sizeof(T));
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  // MV_POISON=<byte>: fill every new device buffer (development check for reads of memory
+  // nothing wrote: results must not change)
+  static const char* poison = std::getenv("MV_POISON");
+  if (e == hipSuccess && poison)
+    e = hipMemset(*p, std::atoi(poison) & 0xFF, n * sizeof(T));
+  return e;
 }
 
 template <class T>
@@ -98,7 +104,7 @@ struct mv_engine {
     if (xml) (void)hipFree(xml);
     xml = nullptr;
     xml_cap = 0;
-    hipError_t e = hipMalloc((void**)&xml, need * sizeof(float));
+    hipError_t e = dalloc(&xml, need);
     if (e == hipSuccess) xml_cap = need;
     return e;
   }
@@ -789,7 +795,10 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     if (r.out_map) r.out_map += b0 * r.n;
     if (r.F) r.F += b0 * r.out_rows * 3;
     if (r.hist) r.hist += b0 * (size_t)r.hist_rows * r.hist_w;
-    r.xml += b0 * (size_t)r.n * Dm4;
+    // Each group owns xml rows [b0, b1) x max(P, O): one group's initial evaluation (n = P)
+    // may still be reading its rows while a faster group already writes its first
+    // offspring (n = O), so the regions must not depend on the phase's n.
+    r.xml += b0 * (size_t)(P > O ? P : O) * Dm4;
     return r;
   };
   auto group_surv = [&](SurvArgs s, int q) {
