@@ -121,7 +121,8 @@ int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* st
  * Outputs dev: survivors [B][n_survive] (merged indices, new population order),
  * rank [B][N] (front index, -1 = unranked) and, for the fronts-ordered individuals
  * (order [B][N], count n_ranked [B]): niche [B][N], dist [B][N].  Any output may be NULL
- * except survivors.  Requires N <= 512, R <= 640. */
+ * except survivors.  Requires N <= 1024 (above 512 the dominance bitsets live in an HBM
+ * scratch), R <= 640. */
 int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t R,
                const double* ref_points, double mu, uint64_t seed, int32_t gen,
                double* ideal, double* worst, double* extreme, int32_t* has_extreme,
@@ -207,7 +208,7 @@ int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
 /* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
 int mv_attack_history(mv_engine* e, double* hist, void* stream);
 /* Per-kernel timing of the last mv_attack_run when enabled: HIP events recorded on the
- * run's stream around k_vary, k_mlp and k_survive of every generation (summed ms). */
+ * run's stream around k_gen, k_cons, k_mlp2 and k_survive of every generation (summed ms). */
 int mv_set_profiling(mv_engine* e, int32_t enabled);
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations);
@@ -215,6 +216,12 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
  * (constraints + f3), ms[2] k_mlp (classifier, f1), ms[3] k_survive (survival + next
  * tournament), summed over the profiled generations. */
 int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
+
+/* The engine's pow for the variation operators (host build of csrc/detmath.h det_pow, the
+ * same IEEE operation sequence as the device code): out[i] = det_pow(x[i], y[i]) for host
+ * arrays.  Replaces np.power in softmax_mutation.py:77-103 (polynomial mutation) and the
+ * SBX option's calc_betaq; oracle/device_order.py:det_pow restates it. */
+int mv_det_pow(int64_t n, const double* x, const double* y, double* out);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/moeva_mi355x.h"
+#include "detmath.h"
 #include "engine.h"
 #include "kernels.h"
 
@@ -1013,6 +1014,12 @@ int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole) {
                  "all %.0f\n", acc[0] / e->B / g, acc[1] / e->B / g, acc[2] / e->B / g,
                  acc[3] / e->B / g);
   }
+  return MV_OK;
+}
+
+int mv_det_pow(int64_t n, const double* x, const double* y, double* out) {
+  if (n < 0 || (n > 0 && (!x || !y || !out))) return fail(MV_ERR_ARG, "bad mv_det_pow arguments");
+  for (int64_t i = 0; i < n; ++i) out[i] = det_pow(x[i], y[i]);
   return MV_OK;
 }
 

@@ -150,7 +150,10 @@ struct SurvArgs {
 };
 
 // Whole attack in one launch (attack.hip) -----------------------------------------------
-constexpr int ATT_T = 256;      // threads per whole-attack workgroup (two workgroups per CU)
+#ifndef MV_ATT_T
+#define MV_ATT_T 256
+#endif
+constexpr int ATT_T = MV_ATT_T;  // threads per whole-attack workgroup (two workgroups per CU)
 constexpr int ATT_SLOTS = 8;    // constant-memory argument slots per device
 struct AttackArgs {
   RowsArgs ev;              // initial evaluation: mode 0, n = P, pool slots 0..P-1

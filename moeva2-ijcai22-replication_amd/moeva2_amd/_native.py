@@ -28,6 +28,7 @@ EXPORTED = [
     "mv_set_crossover",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
+    "mv_det_pow",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -106,6 +107,7 @@ def lib():
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
             "mv_objcalc_create": [C.c_int32, C.POINTER(ObjCalcDesc), C.POINTER(vp)],
             "mv_objcalc_run": [vp, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp, vp, vp],
+            "mv_det_pow": [C.c_int64, _f64p, _f64p, _f64p],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -124,6 +126,16 @@ def lib():
 def check(rc: int):
     if rc != 0:
         raise NativeError(f"libmoeva_mi355x error {rc}: {lib().mv_last_error().decode()}")
+
+
+def det_pow(x, y) -> np.ndarray:
+    """The engine's variation pow (csrc/detmath.h), host build: elementwise, broadcast."""
+    x, y = np.broadcast_arrays(np.asarray(x, np.float64), np.asarray(y, np.float64))
+    x, y = np.ascontiguousarray(x), np.ascontiguousarray(y)
+    out = np.empty(x.shape, np.float64)
+    f64 = lambda a: a.ctypes.data_as(_f64p)  # noqa: E731
+    check(lib().mv_det_pow(x.size, f64(x), f64(y), f64(out)))
+    return out
 
 
 def _ptr(t):

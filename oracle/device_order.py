@@ -28,12 +28,143 @@ and the device attack can be compared trajectory for trajectory:
 
 Every element value (each constraint column, each scaled feature) is the oracle's own; only
 the order of the sums is the engine's.
+
+* pow in the variation operators: ``det_pow`` restates csrc/detmath.h operation for
+  operation (np.power and the device library's pow each round within about an ulp but
+  not identically; run_attack(..., pow_fn=det_pow) gives the engine's mutated genes).
 """
 import numpy as np
 
 from . import moeva_oracle as mo
 
 MV_OP_ABS_SUMDIFF = 3
+
+# fdlibm e_log.c / e_exp.c constants (csrc/detmath.h)
+_LN2_HI, _LN2_LO = 6.93147180369123816490e-01, 1.90821492927058770002e-10
+_LG = (6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01,
+       2.222219843214978396e-01, 1.818357216161805012e-01, 1.531383769920937332e-01,
+       1.479819860511658591e-01)
+_INVLN2 = 1.44269504088896338700e+00
+_P = (1.66666666666666019037e-01, -2.77777777770155933842e-03, 6.61375632143793436117e-05,
+      -1.65339022054652515390e-06, 4.13813679705723846039e-08)
+
+
+def _split(a):
+    t = 134217729.0 * a
+    hi = t - (t - a)
+    return hi, a - hi
+
+
+def _two_prod(a, b):
+    ah, al = _split(a)
+    bh, bl = _split(b)
+    p = a * b
+    return p, ((ah * bh - p) + ah * bl + al * bh) + al * bl
+
+
+def _two_sum(a, b):
+    s = a + b
+    bb = s - a
+    return s, (a - (s - bb)) + (b - bb)
+
+
+def _fast_two_sum(a, b):
+    s = a + b
+    return s, b - (s - a)
+
+
+def _dd_mul(ah, al, bh, bl):
+    p, e = _two_prod(ah, bh)
+    e = e + (ah * bl + al * bh)
+    return _fast_two_sum(p, e)
+
+
+def det_log2(x):
+    """csrc/detmath.h det_log2: ln x as (hi, lo) for x > 0 finite."""
+    m, e = np.frexp(np.asarray(x, np.float64))
+    sm = m < 0.7071067811865476
+    m = np.where(sm, m * 2.0, m)
+    k = (e - sm.astype(e.dtype)).astype(np.float64)
+    f = m - 1.0
+    s = f / (2.0 + f)
+    z = s * s
+    w = z * z
+    L1, L2, L3, L4, L5, L6, L7 = _LG
+    t1 = w * (L2 + w * (L4 + w * L6))
+    t2 = z * (L1 + w * (L3 + w * (L5 + w * L7)))
+    R = t2 + t1
+    hfsq = 0.5 * f * f
+    hi, e1 = _two_sum(k * _LN2_HI, f)
+    lo = ((k * _LN2_LO - hfsq) + s * (hfsq + R)) + e1
+    return hi, lo
+
+
+def det_exp2(th, tl):
+    """csrc/detmath.h det_exp2: exp(th + tl), elementwise."""
+    with np.errstate(over="ignore", invalid="ignore"):
+        kd = np.floor(_INVLN2 * th + 0.5)
+        hi = th - kd * _LN2_HI
+        lo = kd * _LN2_LO - tl
+        r = hi - lo
+        q = r * r
+        P1, P2, P3, P4, P5 = _P
+        c = r - q * (P1 + q * (P2 + q * (P3 + q * (P4 + q * P5))))
+        y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi)
+        kk = np.where(np.isfinite(kd), kd, 0.0).astype(np.int64)
+        out = np.ldexp(y, kk)
+    out = np.where(th > 7.09782712893383973096e+02, np.inf, out)
+    out = np.where(th < -7.45133219101941108420e+02, 0.0, out)
+    return np.where(np.isnan(th), th, out)
+
+
+def _int_pow(x, n, neg):
+    """det_pow's integer branch (n = |y| <= 64) for positive finite x."""
+    _, ex = np.frexp(x)
+    big = np.abs(ex) * n > 900
+    r = np.ones_like(x)
+    b = x.copy()
+    rh, rl, bh, bl = np.ones_like(x), np.zeros_like(x), x.copy(), np.zeros_like(x)
+    m = n
+    while m:
+        if m & 1:
+            r = r * b
+            rh, rl = _dd_mul(rh, rl, bh, bl)
+        m >>= 1
+        if m:
+            b = b * b
+            bh, bl = _dd_mul(bh, bl, bh, bl)
+    if not neg:
+        return np.where(big, r, rh)
+    q = 1.0 / rh
+    p, pe = _two_prod(q, rh)
+    rem = ((1.0 - p) - pe) - q * rl
+    return np.where(big, 1.0 / r, q + rem / rh)
+
+
+def det_pow(x, y):
+    """csrc/detmath.h det_pow, elementwise (y broadcast against x)."""
+    x, y = np.broadcast_arrays(np.asarray(x, np.float64), np.asarray(y, np.float64))
+    with np.errstate(all="ignore"):
+        xs = np.where((x > 0) & np.isfinite(x), x, 1.0)
+        lh, ll = det_log2(xs)
+        th, tl0 = _two_prod(y, lh)
+        tl = tl0 + y * ll
+        th, tl = _fast_two_sum(th, tl)
+        out = det_exp2(th, tl)
+        yi = (y == np.floor(y)) & (np.abs(y) <= 64.0)
+        if yi.any():
+            ay = np.where(yi, np.abs(y), 0.0).astype(np.int64)
+            for n in np.unique(ay[yi]):
+                for neg in (False, True):
+                    sel = yi & (ay == n) & ((y < 0) == neg)
+                    if sel.any():
+                        out[sel] = _int_pow(xs[sel], int(n), neg)
+        out = np.where(x == np.inf, np.where(y > 0, np.inf, 0.0), out)
+        out = np.where(x == 0.0, np.where(y > 0, 0.0, np.inf), out)
+        out = np.where(x < 0.0, np.nan, out)
+        out = np.where((y == 0.0) | (x == 1.0), 1.0, out)
+        out = np.where(np.isnan(x) | np.isnan(y), x + y, out)
+    return out
 
 
 def _fma32(a, b, c):

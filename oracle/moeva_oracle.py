@@ -783,10 +783,11 @@ def sbx_draws(n_matings, V, seed, gen, stream_key=0):
     return (w0 & 1) == 0, (w0 & 2) != 0, px.u53(w1, w2)
 
 
-def sbx_pair(p0, p1, xl, xu, rand, swap, eta):
+def sbx_pair(p0, p1, xl, xu, rand, swap, eta, pow_fn=np.power):
     """pymoo 0.4.2.2 SimulatedBinaryCrossover._do [pymoo-recall] on aligned arrays: the two
     children (c[0], c[1]) where every variable crosses (the caller masks), clipped to the
-    bounds (set_to_bounds_if_outside_by_problem)."""
+    bounds (set_to_bounds_if_outside_by_problem).  ``pow_fn``: np.power (the reference) or
+    oracle.device_order.det_pow (the engine's)."""
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         y1 = np.minimum(p0, p1)
         y2 = np.maximum(p0, p1)
@@ -794,10 +795,10 @@ def sbx_pair(p0, p1, xl, xu, rand, swap, eta):
         delta = np.where(delta < 1.0e-10, 1.0e-10, delta)
 
         def calc_betaq(beta):
-            alpha = 2.0 - np.power(beta, -(eta + 1.0))
+            alpha = 2.0 - pow_fn(beta, -(eta + 1.0))
             mask = rand <= (1.0 / alpha)
-            return np.where(mask, np.power((rand * alpha), (1.0 / (eta + 1.0))),
-                            np.power((1.0 / (2.0 - rand * alpha)), (1.0 / (eta + 1.0))))
+            return np.where(mask, pow_fn((rand * alpha), (1.0 / (eta + 1.0))),
+                            pow_fn((1.0 / (2.0 - rand * alpha)), (1.0 / (eta + 1.0))))
 
         beta = 1.0 + (2.0 * (y1 - xl) / delta)
         c1 = 0.5 * ((y1 + y2) - calc_betaq(beta) * delta)
@@ -810,7 +811,7 @@ def sbx_pair(p0, p1, xl, xu, rand, swap, eta):
 
 
 def sbx_crossover(parents_X, masks_by_type, xl, xu, seed, gen, eta=30.0, prob=0.9,
-                  stream_key=0):
+                  stream_key=0, pow_fn=np.power):
     """MixedVariableCrossover with real_sbx / int_sbx (north_star's SBX option; the
     reference's stale comment moeva2.py:87 names prob 0.9, eta 30): per subset the
     mating-level draw of crossover_draws (prob), then SBX per variable; int_sbx =
@@ -830,7 +831,7 @@ def sbx_crossover(parents_X, masks_by_type, xl, xu, seed, gen, eta=30.0, prob=0.
         p0, p1 = X[0][:, idx], X[1][:, idx]
         lo, hi = xl[idx][None, :], xu[idx][None, :]
         wl, wu = (lo, hi) if subset == 0 else (lo - INT_WIDEN, hi + INT_WIDEN)
-        c0, c1 = sbx_pair(p0, p1, wl, wu, rand[:, idx], swap[:, idx], eta)
+        c0, c1 = sbx_pair(p0, p1, wl, wu, rand[:, idx], swap[:, idx], eta, pow_fn)
         cross = var_on[:, idx] & (np.abs(p0 - p1) > 1.0e-14) & do[:, None]
         c0 = np.where(cross, c0, p0)
         c1 = np.where(cross, c1, p1)
@@ -842,9 +843,10 @@ def sbx_crossover(parents_X, masks_by_type, xl, xu, seed, gen, eta=30.0, prob=0.
     return out.reshape(-1, V)
 
 
-def polynomial_mutation(X, xl, xu, eta, do_mutation, rand):
+def polynomial_mutation(X, xl, xu, eta, do_mutation, rand, pow_fn=np.power):
     """softmax_mutation.py:60-108 (pymoo PolynomialMutation._do) without the softmax.
-    ``do_mutation`` (n, V) bool and ``rand`` (n_mutated,) are the two np.random draws."""
+    ``do_mutation`` (n, V) bool and ``rand`` (n_mutated,) are the two np.random draws.
+    ``pow_fn``: np.power (the reference) or oracle.device_order.det_pow (the engine's)."""
     X = np.asarray(X, np.float64)
     Y = np.full(X.shape, np.inf)
     Y[:, :] = X
@@ -858,12 +860,12 @@ def polynomial_mutation(X, xl, xu, eta, do_mutation, rand):
         mask = rand <= 0.5
         deltaq = np.zeros(Xm.shape)
         xy = 1.0 - delta1
-        val = 2.0 * rand + (1.0 - 2.0 * rand) * (np.power(xy, (eta + 1.0)))
-        d = np.power(val, mut_pow) - 1.0
+        val = 2.0 * rand + (1.0 - 2.0 * rand) * (pow_fn(xy, (eta + 1.0)))
+        d = pow_fn(val, mut_pow) - 1.0
         deltaq[mask] = d[mask]
         xy = 1.0 - delta2
-        val = 2.0 * (1.0 - rand) + 2.0 * (rand - 0.5) * (np.power(xy, (eta + 1.0)))
-        d = 1.0 - (np.power(val, mut_pow))
+        val = 2.0 * (1.0 - rand) + 2.0 * (rand - 0.5) * (pow_fn(xy, (eta + 1.0)))
+        d = 1.0 - (pow_fn(val, mut_pow))
         deltaq[~mask] = d[~mask]
         _Y = Xm + deltaq * (xu_ - xl_)
     _Y[_Y < xl_] = xl_[_Y < xl_]
@@ -916,7 +918,7 @@ def mutation_draws(n_off, V, seed, gen, stream_key=0):
     return do, u[do]
 
 
-def mutation(X, xl, xu, types, seed, gen, eta=20.0, stream_key=0):
+def mutation(X, xl, xu, types, seed, gen, eta=20.0, stream_key=0, pow_fn=np.power):
     """MixedVariableMutation (moeva2.py:104-111): real_pm / int_pm, eta=20.
     int_pm = IntegerFromFloatMutation [pymoo-recall]: bounds widened by 0.5-1e-16,
     np.round (half to even) afterwards.  Build choice: the rounded value is clamped to
@@ -929,7 +931,7 @@ def mutation(X, xl, xu, types, seed, gen, eta=20.0, stream_key=0):
     xu = np.asarray(xu, np.float64)
     wl = np.where(is_int, xl - INT_WIDEN, xl)
     wu = np.where(is_int, xu + INT_WIDEN, xu)
-    Y = polynomial_mutation(X, wl, wu, eta, do, u)
+    Y = polynomial_mutation(X, wl, wu, eta, do, u, pow_fn)
     Yi = np.round(Y)
     Yi = np.minimum(np.maximum(Yi, xl[None, :]), xu[None, :])
     return np.where(is_int[None, :], Yi, Y)
@@ -957,9 +959,11 @@ def initial_population(prob: Problem, pop_size: int) -> np.ndarray:
 
 def run_attack(prob: Problem, ref_points, n_gen, pop_size, n_offsprings, seed, mu=0.05,
                save_history=None, stream_key=0, crossover_kind="two_point", sbx_eta=30.0,
-               evaluate_fn=None):
+               evaluate_fn=None, pow_fn=np.power):
     """evaluate_fn(prob, genes, return_g=True) -> (F, G): default ``evaluate`` (numpy's
-    summation orders); oracle.device_order.evaluate_device_order gives the engine's."""
+    summation orders); oracle.device_order.evaluate_device_order gives the engine's.
+    pow_fn: the variation operators' pow -- np.power (the reference) or
+    oracle.device_order.det_pow (the engine's)."""
     evaluate_fn = evaluate_fn or evaluate
     asp = np.full((1, 3), 1.0 / 3.0)
     gl, gu = genetic_bounds(prob.lay, prob.xl, prob.xu)
@@ -976,11 +980,11 @@ def run_attack(prob: Problem, ref_points, n_gen, pop_size, n_offsprings, seed, m
         par = tournament_parents(X.shape[0], n_offsprings, seed, g, stream_key)
         pX = np.stack([X[par[:, 0]], X[par[:, 1]]])
         if crossover_kind == "sbx":
-            off = sbx_crossover(pX, masks, gl, gu, seed, g, sbx_eta, 0.9, stream_key)
+            off = sbx_crossover(pX, masks, gl, gu, seed, g, sbx_eta, 0.9, stream_key, pow_fn)
         else:
             off = crossover(pX, masks, seed, g, stream_key)
         off = off[:n_offsprings]
-        off = mutation(off, gl, gu, types, seed, g, stream_key=stream_key)
+        off = mutation(off, gl, gu, types, seed, g, stream_key=stream_key, pow_fn=pow_fn)
         Fo, Go = evaluate_fn(prob, off, return_g=True)
         _hist_add(hist, save_history, Fo, Go)
         mX = np.concatenate([X, off])

@@ -11,9 +11,9 @@ same configuration and compares the success rates (north_star: within 1 pp).
 
 The objectives are evaluated in the engine's summation orders (oracle/device_order.py:
 same element values as the reference restatement, the classifier / distance / constraint
-sums in the order the HIP kernels use), so the oracle's attack and the device attack follow
-the same trajectories unless a rare fp32 double rounding or an ulp of pow() flips a
-comparison.  The success rates of the numpy-order oracle (moeva_oracle.evaluate) at the same
+sums in the order the HIP kernels use) and the variation operators use the engine's pow
+(oracle/device_order.py:det_pow = csrc/detmath.h), so the oracle's attack and the device
+attack follow the same trajectories unless a rare fp32 double rounding flips a comparison.  The success rates of the numpy-order oracle (moeva_oracle.evaluate) at the same
 seed are kept in the fixture as ``success_rate_numpy_order`` (NUMPY_ORDER below).
 
     python tests/golden/make_e2e.py botnet_rq1     # 387 states x 1000 gens (~40 min, 8 cores)
@@ -70,8 +70,11 @@ def _init(project):
 
 
 def digest(X: np.ndarray) -> int:
-    """First 8 bytes of the sha256 of the final population's genes (float64, C order)."""
-    h = hashlib.sha256(np.ascontiguousarray(X, np.float64).tobytes()).digest()
+    """First 8 bytes of the sha256 of the final population's genes (float64, C order), with
+    -0.0 canonicalised to +0.0 (x + 0.0): the engine and numpy may produce either sign of a
+    zero gene (e.g. np.rint of a small negative), which compare equal."""
+    X = np.ascontiguousarray(X, np.float64) + 0.0
+    h = hashlib.sha256(X.tobytes()).digest()
     return int.from_bytes(h[:8], "little") & 0x7FFFFFFFFFFFFFFF
 
 
@@ -88,7 +91,7 @@ def one_state(args):
         return do.evaluate_device_order(prob, genes, _CODES, return_g)
 
     r = mo.run_attack(p.problem(p.x[b], norm=2), ref, n_gen, n_pop + 3, n_off, seed,
-                      evaluate_fn=ev)
+                      evaluate_fn=ev, pow_fn=do.det_pow)
     x_f = mo.genetic_to_ml(p.lay, r.pop_X, p.x[b])
     sc, mn = p.ml
     obj = mo.objectives_calc(p.x[b], x_f, p.constraints, p.types, sc, mn, p.weights, p.biases,
@@ -99,7 +102,7 @@ def one_state(args):
 
 def main(name, procs=None):
     project, B, n_gen, n_pop, n_off, seed, eps, thr = CONFIGS[name]
-    procs = procs or os.cpu_count()
+    procs = procs or int(os.environ.get("E2E_PROCS", os.cpu_count()))
     t0 = time.time()
     resp = np.zeros((B, 7), bool)
     best = np.zeros(B)
@@ -116,6 +119,7 @@ def main(name, procs=None):
                         best_f1=best, pop_digest=dig, success_rate=resp.mean(axis=0),
                         success_rate_numpy_order=np.asarray(NUMPY_ORDER[name]),
                         evaluation_order="engine (oracle/device_order.py)",
+                        variation_pow="det_pow (oracle/device_order.py = csrc/detmath.h)",
                         cpu_seconds=time.time() - t0, procs=procs)
     print(name, "success rates o1..o7", resp.mean(axis=0), f"{time.time() - t0:.0f} s")
 

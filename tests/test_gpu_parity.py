@@ -346,7 +346,10 @@ def test_tournament_selection_vs_oracle(P, O):
 def test_variation_vs_oracle(name, kind):
     """Crossover + mutation of the device (k_gen) against the oracle on identical parents and
     Philox draws: two-point (the reference's operator, moeva2.py:90-101) and the SBX option
-    (north_star; real_sbx / int_sbx with eta 30).  Integer genes exact, real genes 1e-12."""
+    (north_star; real_sbx / int_sbx with eta 30).  Against the reference-faithful oracle
+    (np.power): integer genes exact, real genes 1e-12; against the oracle with the engine's
+    pow (device_order.det_pow): every gene bit-identical."""
+    from oracle.device_order import det_pow
     from moeva2_amd.problem import get_engine
 
     p = Project(name)
@@ -386,9 +389,14 @@ def test_variation_vs_oracle(name, kind):
             ref = mo.sbx_crossover(pX, masks, gls[b], gus[b], 99, 5, 30.0, 0.9)[:O]
         else:
             ref = mo.crossover(pX, masks, 99, 5)[:O]
-        ref = mo.mutation(ref, gls[b], gus[b], types, 99, 5)
-        np.testing.assert_array_equal(got[b][:, ~isr], ref[:, ~isr])
-        np.testing.assert_allclose(got[b][:, isr], ref[:, isr], rtol=1e-12, atol=1e-12)
+        ref_np = mo.mutation(ref, gls[b], gus[b], types, 99, 5)
+        np.testing.assert_array_equal(got[b][:, ~isr], ref_np[:, ~isr])
+        np.testing.assert_allclose(got[b][:, isr], ref_np[:, isr], rtol=1e-12, atol=1e-12)
+        if kind == "sbx":
+            ref = mo.sbx_crossover(pX, masks, gls[b], gus[b], 99, 5, 30.0, 0.9,
+                                   pow_fn=det_pow)[:O]
+        ref_det = mo.mutation(ref, gls[b], gus[b], types, 99, 5, pow_fn=det_pow)
+        np.testing.assert_array_equal(got[b], ref_det)
     if kind == "sbx":  # the option changes the children (and keeps them in bounds)
         cx2 = mo.crossover(np.stack([pops[0][parents[:, 0]], pops[0][parents[:, 1]]]), masks,
                            99, 5)[:O]
