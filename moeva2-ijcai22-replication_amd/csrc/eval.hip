@@ -81,6 +81,101 @@ hipError_t release_rows(int slot, hipStream_t stream) {
   return hipEventRecord(g_rings[dev].ev[slot], stream);
 }
 
+// The draws of one offspring row (one row per lane): packed parents (own | oth << 16), the
+// two crossover subsets' draws, and the mutations -- count | overflow << 3 | (last position
+// + 1) << 4, positions and mutated values (crossed parent value through mutate_gene).
+// (A separate one-row-per-lane kernel computing these ahead of k_gen was measured slower:
+// its serial Philox / pow chains sit on the generation's critical path.)
+template <int CAP>
+__device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, const int b,
+                                          const int irow, const bool mine, const int gen,
+                                          const bool sbx, const uint32_t* geo, const int* ginfo,
+                                          const double* gin, const Rng& rng, int& par_v,
+                                          int& cx0_v, int& cx1_v, int& mut_v, int (&mpos)[CAP],
+                                          double (&mval)[CAP]) {
+  const int V = p.V;
+  if (mine) {
+    const int nm = a.n / 2;
+    const int m = irow % nm;
+    const int side = irow / nm;
+    const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
+    par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
+    cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
+    cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
+    if (sbx) {  // SBX: the subsets' mating-level draws only (no segment)
+      cx0_v &= 1;
+      cx1_v &= 1;
+    }
+  }
+  // (1) mutation positions and their PM uniforms
+  const float lq = __log2f(1.0f - 1.0f / (float)V);
+#ifdef MV_DBG_NOMUT
+  bool going = false;  // development: prologue cost without mutations (results wrong)
+#else
+  bool going = mine && !sbx;
+#endif
+  int pos = -1, cnt = 0, ovf = 0;
+  double mu[CAP] = {};
+#pragma unroll 1
+  for (int j = 0; j <= CAP && __ballot(going); ++j) {
+    bool have = false;
+    double u = 0.0;
+    if (going) {
+      const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+      pos += 1 + geo_gap(geo, V, w.x, lq);
+      if (pos >= V) {
+        going = false;
+      } else if (j == CAP) {
+        ovf = 1;
+        going = false;
+      } else {
+        have = true;
+        u = u53(w.y, w.z);
+        cnt = j + 1;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CAP; ++q)
+      if (have && q == j) {
+        mpos[q] = pos;
+        mu[q] = u;
+      }
+  }
+  // (2) + (3) one (row, mutation) pair per lane: lane 4 k + q loads row k's crossed parent
+  // value and gene bounds at its q-th mutated position and mutates it -- one pow pair deep
+  // instead of a loop over the wave's largest mutation count (a wave holds <= 16 rows).
+  static_assert(CAP == 4, "row_draws maps 16 rows x 4 mutations onto the 64 lanes");
+  const double* gl = a.s.gl + (size_t)b * V;
+  const double* gu = a.s.gu + (size_t)b * V;
+  const int lane = threadIdx.x & 63;
+  const int kk = lane >> 2, qq = lane & 3;
+  int pq = -1;
+  double uq = 0.0;
+#pragma unroll
+  for (int q = 0; q < CAP; ++q) {
+    const int pv = __shfl(mpos[q], kk);
+    const double uv = __shfl(mu[q], kk);
+    if (q == qq) {
+      pq = pv;
+      uq = uv;
+    }
+  }
+  const int cntk = __shfl(cnt, kk), park = __shfl(par_v, kk);
+  const int c0k = __shfl(cx0_v, kk), c1k = __shfl(cx1_v, kk);
+  const int mp = pq < 0 ? 0 : pq;  // unconditional, clamped loads
+  const int gi = ginfo[mp];
+  double xv = gin[(size_t)(swapped_packed(gi, c0k, c1k) ? (park >> 16) : (park & 0xFFFF)) * V + mp];
+  const double lo = gl[mp], hi = gu[mp];
+  if (qq < cntk) xv = mutate_gene(xv, lo, hi, (gi & 3) == 0, uq, a.eta);
+#pragma unroll
+  for (int q = 0; q < CAP; ++q) mval[q] = __shfl(xv, (lane * 4 + q) & 63);  // back to row lanes
+  int last = -1;
+#pragma unroll
+  for (int q = 0; q < CAP; ++q)
+    if (q < cnt) last = mpos[q];
+  mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
+}
+
 // k_gen: variation (mode 1) or gene load (mode 0), the child genes to the pool, the fp32
 // ML-scaled mutable row for k_mlp (default_problem.py:119-121) and f2, the encoder-MinMax
 // distance (default_problem.py:80-91).
@@ -173,87 +268,8 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
   const int irow = rc.i0 + wave + 4 * lane;
   if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
   if (a.mode == 1) {
-        if (mine) {
-      const int nm = a.n / 2;
-      const int m = irow % nm;
-      const int side = irow / nm;
-      const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
-      par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
-      cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
-      cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
-      if (sbx) {  // SBX: the subsets' mating-level draws only (no segment)
-        cx0_v &= 1;
-        cx1_v &= 1;
-      }
-    }
-    // (1) mutation positions and their PM uniforms
-    const float lq = __log2f(1.0f - 1.0f / (float)V);
-    bool going = mine && !sbx;
-    int pos = -1, cnt = 0, ovf = 0;
-    double mu[MUT_CAP];
-#pragma unroll 1
-    for (int j = 0; j <= MUT_CAP && __ballot(going); ++j) {
-      bool have = false;
-      double u = 0.0;
-      if (going) {
-        const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-        pos += 1 + geo_gap(s_geo, V, w.x, lq);
-        if (pos >= V) {
-          going = false;
-        } else if (j == MUT_CAP) {
-          ovf = 1;
-          going = false;
-        } else {
-          have = true;
-          u = u53(w.y, w.z);
-          cnt = j + 1;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < MUT_CAP; ++q)
-        if (have && q == j) {
-          mpos[q] = pos;
-          mu[q] = u;
-        }
-    }
-    // (2) crossed parent values and gene bounds at those positions: independent,
-    // unconditional loads (clamped position; unused slots are never applied), (3) mutate
-    const double* gl = a.s.gl + (size_t)b * V;
-    const double* gu = a.s.gu + (size_t)b * V;
-    double mlo[MUT_CAP], mhi[MUT_CAP];
-#pragma unroll
-    for (int q = 0; q < MUT_CAP; ++q) {
-      const int mp = mpos[q] < 0 ? 0 : mpos[q];
-      const bool sw = swapped_packed(s_ginfo[mp], cx0_v, cx1_v);
-      mval[q] = gin[(size_t)(sw ? (par_v >> 16) : (par_v & 0xFFFF)) * V + mp];
-      mlo[q] = gl[mp];
-      mhi[q] = gu[mp];
-    }
-#pragma unroll 1
-    for (int q = 0; q < MUT_CAP && __ballot(q < cnt); ++q) {
-      int gp = 0;
-      double xv = 0.0, u = 0.0, lo = 0.0, hi = 0.0;
-#pragma unroll
-      for (int r = 0; r < MUT_CAP; ++r)
-        if (r == q) {
-          gp = mpos[r];
-          xv = mval[r];
-          u = mu[r];
-          lo = mlo[r];
-          hi = mhi[r];
-        }
-      if (q < cnt) {
-        xv = mutate_gene(xv, lo, hi, (s_ginfo[gp] & 3) == 0, u, a.eta);
-#pragma unroll
-        for (int r = 0; r < MUT_CAP; ++r)
-          if (r == q) mval[r] = xv;
-      }
-    }
-    int last = -1;
-#pragma unroll
-    for (int q = 0; q < MUT_CAP; ++q)
-      if (q < cnt) last = mpos[q];
-    mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
+    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
+                       cx1_v, mut_v, mpos, mval);
   } else if (mine) {
     par_v = irow | (irow << 16);
   }
