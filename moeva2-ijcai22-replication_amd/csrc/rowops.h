@@ -495,7 +495,8 @@ __device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
 
 
 constexpr int M2_ROWS = 64;
-constexpr int M2_ALD = 68;  // layer-0 chunk row stride (floats)
+constexpr int M2_ALD = 72;  // layer-0 chunk row stride (floats): 8 mod 64 makes the MFMA A-operand
+                            // ds_read_b128 groups conflict-free (68 was 2-way in half the groups)
 
 __host__ __device__ inline int mlp2_hmax(const DProblem& p) {
   int h = 16;
