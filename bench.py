@@ -92,6 +92,7 @@ def load_states(w):
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector peak)
+MFMA_BF16_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 
 
 def eng_dims(eng):
@@ -217,6 +218,9 @@ def main():
     ap.add_argument("--mode", default="auto", choices=["auto", "chain", "whole"],
                     help="attack schedule: per-phase kernel chain or one whole-attack launch")
     ap.add_argument("--crossover", default="two_point", choices=["two_point", "sbx"])
+    ap.add_argument("--mlp-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="classifier precision: fp32 (parity, default) or the bf16 perf mode "
+                         "(a separately labelled line: f1 is not Keras's value)")
     ap.add_argument("--shard", action="store_true",
                     help="strong scaling: split the states over the ranks")
     ap.add_argument("--cpu-gens", type=int, default=300)
@@ -246,6 +250,8 @@ def main():
     eng, c = build_engine(w, device)
     eng.set_attack_mode(args.mode)
     eng.set_crossover(args.crossover)
+    eng.set_mlp_precision(args.mlp_dtype)
+    bf16 = args.mlp_dtype == "bf16"
     X_all = load_states(w)
     B_all = X_all.shape[0]
     lo, hi = shard_bounds(B_all, world, rank) if args.shard else (0, B_all)
@@ -338,7 +344,7 @@ def main():
     # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
     tpath = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{args.workload}_{args.mode}.json")
-    if os.path.exists(tpath) and args.crossover == "two_point":
+    if os.path.exists(tpath) and args.crossover == "two_point" and not bf16:
         with open(tpath) as fh:
             traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()
                        if isinstance(v, dict) and "traffic_bytes" in v}
@@ -362,14 +368,16 @@ def main():
         mlp_ms = kt["mlp_ms"] / ng
         surv_ms = kt["survive_ms"] / ng
         mlp_tfs = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
+        mlp_peak = MFMA_BF16_PEAK_TFS if bf16 else MFMA_F32_PEAK_TFS
         kernels = {
             "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows,
                          gen_ms, "k_gen"),
             "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
                           "k_cons"),
-            "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": MFMA_F32_PEAK_TFS,
-                      "unit": "TFLOP/s", "frac": mlp_tfs / MFMA_F32_PEAK_TFS,
-                      "traffic": traffic.get("k_mlp"), "kernel": "k_mlp (fp32 MFMA Dense chain)",
+            "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": mlp_peak,
+                      "unit": "TFLOP/s", "frac": mlp_tfs / mlp_peak,
+                      "traffic": traffic.get("k_mlp"),
+                      "kernel": "k_mlp (%s MFMA Dense chain)" % ("bf16" if bf16 else "fp32"),
                       "algorithmic_flops_per_launch": eval_flops * rows,
                       "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},
             "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
@@ -401,7 +409,9 @@ def main():
         "config": {"workload": args.workload, "states": B_all, "states_per_gpu": B,
                    "pop_size": P, "n_offsprings": O, "n_gen": G, "norm": w["norm"],
                    "history": w["history"], "evals_per_state": evals_per_state,
-                   "classifier_dtype": "f32 (MFMA)", "crossover": args.crossover,
+                   "classifier_dtype": ("bf16 perf mode (bf16 MFMA, fp32 accumulate; not a "
+                                        "parity result)" if bf16 else "f32 (MFMA)"),
+                   "crossover": args.crossover,
                    "schedule": "whole-attack kernel" if whole else "per-phase kernel chain",
                    "parallelism": par},
         "attack_wall_clock_per_1k_states_s": elapsed / args.steps / states_total * 1000.0,

@@ -200,6 +200,12 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
 /* 0: auto (default; currently the chain), 1: per-phase kernel chain, 2: whole-attack kernel
  * when the problem layout has an instance (else the chain). */
 int mv_set_attack_mode(mv_engine* e, int32_t mode);
+/* Classifier precision of the engine's fitness path (mv_evaluate, mv_attack_run): 0 = fp32
+ * (default; the parity mode: exact fp32 products on v_mfma_f32_16x16x4f32, as Keras computes
+ * classifier.py:23-29), 1 = bf16 perf mode (hidden-layer weights and activations rounded to
+ * bf16, fp32 accumulation on v_mfma_f32_16x16x32_bf16; f1 is no longer Keras's value, so
+ * results are not parity results).  No reference counterpart: an engine option. */
+int mv_set_mlp_precision(mv_engine* e, int32_t bf16);
 /* Device ms of the last profiled mv_attack_run's k_attack launch (0 if the chain ran) and
  * whether the last run was the whole-attack kernel. */
 int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);

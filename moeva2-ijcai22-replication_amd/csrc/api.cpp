@@ -67,8 +67,17 @@ __global__ void k_fill_i(int* p, size_t n, int v) {
 
 }  // namespace
 
+// fp32 -> bf16 bits, round to nearest even (NaN stays a quiet NaN)
+static unsigned short bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return (unsigned short)((u >> 16) | 0x40);
+  return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
 struct mv_engine {
   int device = 0;
+  int mlp_bf16 = 0;  // bf16 perf mode of the classifier tiles (mv_set_mlp_precision)
   DProblem p{};
   std::vector<void*> prob_allocs;
   float* W1full = nullptr;
@@ -374,6 +383,18 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
           wp[((size_t)(k / 16) * Nl + n) * 16 + (k % 16)] = src[(size_t)k * Nl + n];
       K((float**)&p.Wp[l], wp.data(), wp.size());
     }
+    // bf16 perf mode packing of the MFMA layers: Wb[kg][n][32] = bf16(W[32 kg + i][n]), K
+    // zero padded to a multiple of 32 (engine.h DProblem::Wb)
+    for (int l = 0; l + 1 < md->n_layers; ++l) {
+      const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
+      const int K32 = (Kl + 31) & ~31;
+      const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major
+      std::vector<unsigned short> wb((size_t)K32 * Nl, 0);
+      for (int k = 0; k < Kl; ++k)
+        for (int n = 0; n < Nl; ++n)
+          wb[((size_t)(k / 32) * Nl + n) * 32 + (k % 32)] = bf16_bits(src[(size_t)k * Nl + n]);
+      K((unsigned short**)&p.Wb[l], wb.data(), wb.size());
+    }
   } else {
     p.n_layers = 0;
     e->H1 = 16;
@@ -457,6 +478,7 @@ static RowsArgs base_rows(const mv_engine* e) {
   a.sbx_eta = e->sbx_eta;
   a.mut_thr = (uint32_t)(4294967296.0 / (double)e->p.V);
   a.do_eval = 1;
+  a.p.mlp_bf16 = e->has_model && e->mlp_bf16;
   return a;
 }
 
@@ -680,7 +702,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   int mode = e->attack_mode;
   if (env_mode && std::strcmp(env_mode, "whole") == 0) mode = 2;
   if (env_mode && std::strcmp(env_mode, "chain") == 0) mode = 1;
-  e->last_whole = mode == 2 && attack_supported(e->p, P, O, R);
+  // (the whole-attack kernel's classifier phase is fp32 only: the bf16 mode runs the chain)
+  e->last_whole = mode == 2 && !e->mlp_bf16 && attack_supported(e->p, P, O, R);
   if (e->last_whole) {
     // the whole GA loop in one launch: one workgroup per state (attack.hip)
     AttackArgs A{};
@@ -978,6 +1001,13 @@ int mv_set_crossover(mv_engine* e, int32_t kind, double eta, double prob) {
   e->cx_kind = kind;
   e->sbx_eta = eta;
   e->cx_prob = prob;
+  return MV_OK;
+}
+
+int mv_set_mlp_precision(mv_engine* e, int32_t bf16) {
+  if (!e || bf16 < 0 || bf16 > 1) return fail(MV_ERR_ARG, "mlp precision: 0 (fp32) or 1 (bf16)");
+  if (bf16 && !e->has_model) return fail(MV_ERR_STATE, "no device classifier to run in bf16");
+  e->mlp_bf16 = bf16;
   return MV_OK;
 }
 

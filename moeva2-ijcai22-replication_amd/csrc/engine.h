@@ -71,6 +71,13 @@ struct DProblem {
   // for four 16x16x4 MFMA k-steps
   const float* Wp[MAX_LAYERS];
   int mlp2;               // hidden widths fit k_mlp2 (multiples of 16, <= 128)
+  // bf16 perf mode (mv_set_mlp_precision, opt-in; fp32 is the parity default): the hidden
+  // layers' weights as bf16 bits packed [K/32][N][32] (K zero padded to a multiple of 32:
+  // 32 consecutive k of one output column contiguous, so one dwordx4 is a lane's B operand of
+  // v_mfma_f32_16x16x32_bf16); activations are rounded to bf16 as they are read, fp32
+  // accumulation, final Dense + softmax unchanged
+  const unsigned short* Wb[MAX_LAYERS];
+  int mlp_bf16;
 };
 
 struct DStates {

@@ -530,6 +530,40 @@ __global__ __launch_bounds__(NARROW_T) void k_narrow(int slot, int gen, int hist
   narrow_rows<NV, FULL>(c_rows[slot], gen, hist_row0, smem);
 }
 
+// Epilogue of a dense layer: + bias (per state for layer 0) and ReLU into the LDS tile.
+template <int MAXCT, int RT>
+__device__ __forceinline__ void dense_store(const floatx4 (&acc)[RT][MAXCT], int N,
+                                            const float* __restrict__ bias,
+                                            const float* __restrict__ bias_state,
+                                            const int* row_state, float* __restrict__ out,
+                                            int ldo, int wave, int lane) {
+  const int nct = N >> 4;
+  const int ka = lane >> 4, il = lane & 15;
+#pragma unroll
+  for (int c = 0; c < MAXCT; ++c) {
+    const int ct = wave + c * 4;
+    if (ct < nct) {
+      const int col = ct * 16 + il;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = rt * 16 + ka * 4 + j;
+          float bv;
+          if (bias_state) {
+            const int st = row_state[row] < 0 ? 0 : row_state[row];
+            bv = bias_state[(size_t)st * N + col];
+          } else {
+            bv = bias[col];
+          }
+          const float v = acc[rt][c][j] + bv;
+          out[row * ldo + col] = v > 0.f ? v : 0.f;
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Dense layer on MFMA: out[16 RT][N] = relu(in[16 RT][K] . W[K][N] + bias), K % 4 == 0,
 // N % 16 == 0 (RT = 2: the 32-row tiles of k_mlp / k_predict; RT = 1: k_predict's 16-row
@@ -580,29 +614,55 @@ __device__ __forceinline__ void dense_mfma(const float* __restrict__ in, int ldi
       }
     }
   }
+  dense_store<MAXCT, RT>(acc, N, bias, bias_state, row_state, out, ldo, wave, lane);
+}
+
+// dense_mfma in the bf16 perf mode: k-steps of 32 on v_mfma_f32_16x16x32_bf16, B operands
+// one dwordx4 per lane and column tile of the packed Wb ([K/32][N][32]), A rows read as 8
+// scalars (the tiles' odd row strides are not 16-B aligned) rounded to bf16.  Lane (il, ka)
+// holds k = 32 s + 8 ka + j of step s; k past K contributes zeros.
+template <int MAXCT, int RT = 2>
+__device__ __forceinline__ void dense_mfma_bf(const float* __restrict__ in, int ldi, int K,
+                                              const unsigned short* __restrict__ Wb, int N,
+                                              const float* __restrict__ bias,
+                                              const float* __restrict__ bias_state,
+                                              const int* row_state, float* __restrict__ out,
+                                              int ldo, int wave, int lane) {
+  const int nct = N >> 4;
+  floatx4 acc[RT][MAXCT];
 #pragma unroll
-  for (int c = 0; c < MAXCT; ++c) {
-    const int ct = wave + c * 4;
-    if (ct < nct) {
-      const int col = ct * 16 + il;
+  for (int c = 0; c < MAXCT; ++c)
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
+    for (int r = 0; r < RT; ++r) acc[r][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ka = lane >> 4, il = lane & 15;
+  const __bf16* W = (const __bf16*)Wb;
+  const int nst = (K + 31) >> 5;
+  for (int s = 0; s < nst; ++s) {
+    const int k = 32 * s + 8 * ka;
+    const bool on = k < K;
+    bf16x8 av[RT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = rt * 16 + ka * 4 + j;
-          float bv;
-          if (bias_state) {
-            const int st = row_state[row] < 0 ? 0 : row_state[row];
-            bv = bias_state[(size_t)st * N + col];
-          } else {
-            bv = bias[col];
-          }
-          const float v = acc[rt][c][j] + bv;
-          out[row * ldo + col] = v > 0.f ? v : 0.f;
-        }
+    for (int r = 0; r < RT; ++r) {
+      const float* ar = in + (il + 16 * r) * ldi + (on ? k : 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) av[r][j] = (__bf16)(on ? ar[j] : 0.f);
+    }
+    bf16x8 bv[MAXCT];
+#pragma unroll
+    for (int c = 0; c < MAXCT; ++c) {
+      const int ct = wave + c * 4 < nct ? wave + c * 4 : nct - 1;
+      bv[c] = *(const bf16x8*)(W + ((size_t)s * N + ct * 16 + il) * 32 + 8 * ka);
+    }
+#pragma unroll
+    for (int c = 0; c < MAXCT; ++c) {
+      if (wave + c * 4 < nct) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[r], bv[c], acc[r][c], 0, 0, 0);
       }
     }
   }
+  dense_store<MAXCT, RT>(acc, N, bias, bias_state, row_state, out, ldo, wave, lane);
 }
 
 // Final Dense + softmax for row t (one thread), weights staged in LDS: ws[k*nout + c], wsb[c].
@@ -632,7 +692,7 @@ __host__ __device__ inline int max_hidden(const int* dims, int n_layers) {
 }
 
 // Dense chain over 32-row tiles of the fp32 ML rows -> f1.
-template <int MAXCT>
+template <int MAXCT, bool BF>
 __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -676,8 +736,12 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
   float* other = R1;
   for (int l = 0; l + 1 < nl; ++l) {
     const int N = p.dims[l + 1];
-    dense_mfma<MAXCT>(in, ldi, K, p.W[l], N, p.bias[l], l == 0 ? a.s.bias1 : nullptr, row_state,
-                      outb, N + 1, wave, lane);
+    if (BF)
+      dense_mfma_bf<MAXCT>(in, ldi, K, p.Wb[l], N, p.bias[l], l == 0 ? a.s.bias1 : nullptr,
+                           row_state, outb, N + 1, wave, lane);
+    else
+      dense_mfma<MAXCT>(in, ldi, K, p.W[l], N, p.bias[l], l == 0 ? a.s.bias1 : nullptr,
+                        row_state, outb, N + 1, wave, lane);
     __syncthreads();
     in = outb;
     ldi = N + 1;
@@ -715,7 +779,7 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
 // k_gen through a double-buffered LDS chunk of 64 k (register staged); hidden outputs go to
 // an LDS ping-pong; the immutable features' contribution to layer 0 is the per-state bias
 // bias1 (k_setup_states).  The last Dense + softmax is a dot product per row on the VALU.
-template <int CJ>
+template <int CJ, bool BF>
 __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -776,8 +840,13 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     for (int c = 0; c < nch; ++c) {
       if (c + 1 < nch) M2_CHUNK_LOAD(c + 1)
       const int ng = min(4, nkg0 - 4 * c);
-      mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, p.Wp[0] + (size_t)4 * c * N0 * 16,
-                     ng, N0, acc, tile_map(N0 >> 4, wave), il, ka);
+      if (BF)
+        mlp2_layer_bf<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, 16 * ng, p.Wb[0], 2 * c, N0,
+                          acc, tile_map(N0 >> 4, wave), il, ka);
+      else
+        mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
+                       p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, tile_map(N0 >> 4, wave),
+                       il, ka);
       if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1)
       __syncthreads();
     }
@@ -792,8 +861,12 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
         for (int cj = 0; cj < CJ; ++cj)
 #pragma unroll
           for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-        mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N, acc,
-                       m, il, ka);
+        if (BF)
+          mlp2_layer_bf<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.dims[l], p.Wb[l], 0, N,
+                            acc, m, il, ka);
+        else
+          mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N,
+                         acc, m, il, ka);
       }
       float* out = H + (l & 1) * M2_ROWS * hld;
 #pragma unroll
@@ -1067,8 +1140,10 @@ static void configure_lds_once() {
   static bool done = false;
   if (done) return;
   const int lim = 160 * 1024;
-  const void* fns[] = {(const void*)k_mlp<1>,          (const void*)k_mlp<2>,
-                       (const void*)k_mlp<4>,          (const void*)k_mlp<8>,
+  const void* fns[] = {(const void*)k_mlp<1, false>, (const void*)k_mlp<2, false>,
+                       (const void*)k_mlp<4, false>, (const void*)k_mlp<8, false>,
+                       (const void*)k_mlp<1, true>,  (const void*)k_mlp<2, true>,
+                       (const void*)k_mlp<4, true>,  (const void*)k_mlp<8, true>,
                        (const void*)k_constraints<false>, (const void*)k_constraints<true>};
   for (const void* f : fns)
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -1289,19 +1364,19 @@ static int cu_count() {
   return n;
 }
 
-template <int CJ>
+template <int CJ, bool BF>
 static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static bool configured = false;
   static size_t occ_lds = 0;
   static int occ = 2;
   if (!configured) {
-    allow_lds(k_mlp2<CJ>);
+    allow_lds(k_mlp2<CJ, BF>);
     configured = true;
   }
   const size_t lds = mlp2_lds(a.p);
   if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ>, 256, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF>, 256, lds) != hipSuccess ||
         n < 1)
       n = 1;
     (void)hipGetLastError();
@@ -1310,29 +1385,41 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
   const int grid = ntiles < occ * cu_count() ? ntiles : occ * cu_count();
-  hipLaunchKernelGGL((k_mlp2<CJ>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
+  hipLaunchKernelGGL((k_mlp2<CJ, BF>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
-  if (a.p.mlp2 && !std::getenv("MV_MLP_V1"))
-    return mlp2_hmax(a.p) <= 64 ? mlp2_go<1>(a, slot, hist_row0, stream)
-                                : mlp2_go<2>(a, slot, hist_row0, stream);
+  if (a.p.mlp2 && !std::getenv("MV_MLP_V1")) {
+    if (a.p.mlp_bf16)
+      return mlp2_hmax(a.p) <= 64 ? mlp2_go<1, true>(a, slot, hist_row0, stream)
+                                  : mlp2_go<2, true>(a, slot, hist_row0, stream);
+    return mlp2_hmax(a.p) <= 64 ? mlp2_go<1, false>(a, slot, hist_row0, stream)
+                                : mlp2_go<2, false>(a, slot, hist_row0, stream);
+  }
   configure_lds_once();
   const int nl = a.p.n_layers;
   const int hmax = max_hidden(a.p.dims, nl);
   const size_t lds = mlp_lds_bytes(a.p.Dm4, hmax, a.p.dims[nl - 1], a.p.dims[nl]);
   const dim3 grid((a.total + EVAL_TR - 1) / EVAL_TR);
   const int nct = hmax / 16;
+#define MLP(M)                                                                           \
+  {                                                                                      \
+    if (a.p.mlp_bf16)                                                                    \
+      hipLaunchKernelGGL((k_mlp<M, true>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
+    else                                                                                 \
+      hipLaunchKernelGGL((k_mlp<M, false>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
+  }
   if (nct <= 4)
-    hipLaunchKernelGGL(k_mlp<1>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
+    MLP(1)
   else if (nct <= 8)
-    hipLaunchKernelGGL(k_mlp<2>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
+    MLP(2)
   else if (nct <= 16)
-    hipLaunchKernelGGL(k_mlp<4>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
+    MLP(4)
   else
-    hipLaunchKernelGGL(k_mlp<8>, grid, dim3(EVAL_T), lds, stream, slot, hist_row0);
+    MLP(8)
+#undef MLP
   return hipGetLastError();
 }
 

@@ -585,4 +585,73 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
   }
 }
 
+// bf16 perf mode ------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Eight fp32 activations (two float4) rounded to bf16 (v_cvt_pk_bf16_f32, RNE); zeros when
+// the lane's k lies past the layer's K (the LDS there is not part of the operand).
+__device__ __forceinline__ bf16x8 to_bf16x8(float4 lo, float4 hi, bool on) {
+  bf16x8 r;
+  r[0] = (__bf16)(on ? lo.x : 0.f);
+  r[1] = (__bf16)(on ? lo.y : 0.f);
+  r[2] = (__bf16)(on ? lo.z : 0.f);
+  r[3] = (__bf16)(on ? lo.w : 0.f);
+  r[4] = (__bf16)(on ? hi.x : 0.f);
+  r[5] = (__bf16)(on ? hi.y : 0.f);
+  r[6] = (__bf16)(on ? hi.z : 0.f);
+  r[7] = (__bf16)(on ? hi.w : 0.f);
+  return r;
+}
+
+// mlp2_layer in the bf16 mode: k-steps of 32 on v_mfma_f32_16x16x32_bf16.  Lane (il, ka)
+// holds k = 32 s + 8 ka + j (j < 8) of step s: its A operand is two ds_read_b128 of its row
+// (rounded to bf16), its B operand one dwordx4 of Wb[kg0 + s][n][32].  K (a multiple of 16)
+// is the number of k of A processed here; lanes whose 8 k lie past K contribute zeros.
+template <int CJ>
+__device__ __forceinline__ void mlp2_layer_bf(const float* __restrict__ A, int lda, int K,
+                                              const unsigned short* __restrict__ Wb, int kg0,
+                                              int N, floatx4 (&acc)[CJ][4], TileMap m, int il,
+                                              int ka) {
+  const int nct = N >> 4;
+  const int wave = m.cb;
+  const int nst = (K + 31) >> 5;
+  const __bf16* W = (const __bf16*)Wb;
+  auto load_b = [&](int s, bf16x8 (&bf)[CJ]) {
+    const int sc = s < nst ? s : nst - 1;
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) {
+      const int ct = wave + 4 * cj < nct ? wave + 4 * cj : nct - 1;
+      bf[cj] = *(const bf16x8*)(W + ((size_t)(kg0 + sc) * N + ct * 16 + il) * 32 + 8 * ka);
+    }
+  };
+  bf16x8 bf[CJ];
+  load_b(0, bf);
+  for (int s = 0; s < nst; ++s) {
+    bf16x8 bn[CJ];
+    load_b(s + 1, bn);  // next step's weights (L2) while this step's MFMAs run
+    const int k = 32 * s + 8 * ka;
+    const bool on = k < K;
+    const int kc = on ? k : 0;
+    bf16x8 af[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      const int r = m.rt0 + (rt < m.nrt ? rt : 0);
+      const float* ar = A + (r * 16 + il) * lda + kc;
+      af[rt] = to_bf16x8(*(const float4*)ar, *(const float4*)(ar + 4), on);
+    }
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) {
+      if (wave + 4 * cj < nct) {
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          if (rt >= m.nrt) continue;
+          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bf[cj], acc[cj][rt], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
+  }
+}
+
 }  // namespace mv

@@ -25,7 +25,7 @@ EXPORTED = [
     "mv_set_states", "mv_evaluate", "mv_decode", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
     "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_set_attack_mode",
-    "mv_set_crossover",
+    "mv_set_crossover", "mv_set_mlp_precision",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
     "mv_det_pow",
@@ -102,6 +102,7 @@ def lib():
             "mv_get_phase_times": [vp, _f64p, _i32p],
             "mv_set_attack_mode": [vp, C.c_int32],
             "mv_set_crossover": [vp, C.c_int32, C.c_double, C.c_double],
+            "mv_set_mlp_precision": [vp, C.c_int32],
             "mv_get_attack_time": [vp, _f64p, _i32p],
             "mv_mlp_create": [C.c_int32, C.POINTER(ModelDesc), C.POINTER(vp)],
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
@@ -315,6 +316,14 @@ class Engine:
         """"two_point" (the reference's operator) or "sbx" (SimulatedBinaryCrossover)."""
         check(lib().mv_set_crossover(self._h, {"two_point": 0, "sbx": 1}[kind], float(eta),
                                      float(prob)))
+
+    def set_mlp_precision(self, dtype: str = "fp32"):
+        """Classifier precision of the fitness path: "fp32" (parity default) or "bf16" (perf
+        mode: bf16 weights/activations on bf16 MFMA, fp32 accumulation)."""
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"mlp dtype {dtype!r}: 'fp32' or 'bf16'")
+        check(lib().mv_set_mlp_precision(self._h, 1 if dtype == "bf16" else 0))
+        self.mlp_dtype = dtype
 
     def set_attack_mode(self, mode: str):
         """"chain": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per

@@ -48,7 +48,7 @@ class Moeva2:
                  problem_class=None, l2_ball_size=0.1, norm=np.inf, n_gen=625, n_pop=640,
                  n_offsprings=320, scale_objectives=True, save_history=False, seed=None,
                  n_jobs=-1, verbose=1, device: int = 0, crossover: str = "two_point",
-                 sbx_eta: float = 30.0) -> None:
+                 sbx_eta: float = 30.0, mlp_dtype: str = "fp32") -> None:
         self._classifier_path = classifier_path
         self._constraints = constraints
         self._ml_scaler = ml_scaler
@@ -72,6 +72,11 @@ class Moeva2:
             raise ValueError(f"crossover must be 'two_point' or 'sbx', got {crossover!r}")
         self._crossover = crossover
         self._sbx_eta = sbx_eta
+        # engine extension: classifier precision, "fp32" (Keras's arithmetic, the parity
+        # mode) or "bf16" (perf mode on bf16 MFMA; f1 no longer matches Keras)
+        if mlp_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"mlp_dtype must be 'fp32' or 'bf16', got {mlp_dtype!r}")
+        self._mlp_dtype = mlp_dtype
         self._classifier = None
         self.last_engine = None
 
@@ -110,6 +115,7 @@ class Moeva2:
         eng = get_engine(self._constraints, clf, self._ml_scaler, self.norm,
                          self._scale_objectives, self.device)
         eng.set_crossover(self._crossover, self._sbx_eta)
+        eng.set_mlp_precision(self._mlp_dtype)
         bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
         xl = np.array([b[0] for b in bounds], np.float64)
         xu = np.array([b[1] for b in bounds], np.float64)

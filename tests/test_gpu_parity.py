@@ -205,6 +205,105 @@ def test_wide_mlp_config_matches_fp32_reference():
     np.testing.assert_array_equal(Fe.cpu().numpy(), outs[0][1])
 
 
+# ------------------------------------------------------------------ bf16 perf mode
+def _bf16(a):
+    """fp32 -> bf16 -> fp32, round to nearest even (v_cvt_pk_bf16_f32 on finite values)."""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def _bf16_forward(x_ml, mut, W, bs):
+    """The engine's bf16 perf-mode classifier restated in numpy: layer 1 over the mutable
+    features with bf16 weights/activations and the immutable features folded into an fp32
+    per-row bias (k_setup_states), hidden layers bf16 x bf16 with fp32 accumulation, final
+    Dense + softmax in fp32 (test infrastructure, not an oracle of the reference)."""
+    x = np.asarray(x_ml, np.float64).astype(np.float32)
+    imm = np.setdiff1d(np.arange(x.shape[1]), mut)
+    bias1 = bs[0].astype(np.float32) + x[:, imm].astype(np.float64) @ W[0][imm].astype(np.float64)
+    h = _bf16(x[:, mut]).astype(np.float64) @ _bf16(W[0][mut]).astype(np.float64) + bias1
+    h = np.maximum(h.astype(np.float32), 0)
+    for w, b in zip(W[1:-1], bs[1:-1]):
+        h = _bf16(h).astype(np.float64) @ _bf16(w).astype(np.float64) + b
+        h = np.maximum(h.astype(np.float32), 0)
+    z = h.astype(np.float64) @ W[-1].astype(np.float64) + bs[-1]
+    z = z - z.max(axis=1, keepdims=True)
+    e = np.exp(z)
+    return e / e.sum(axis=1, keepdims=True)
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_bf16_mode_classifier(wide):
+    """mv_set_mlp_precision(bf16): k_mlp2 (shipped botnet net) / k_mlp (configs[4] wide net)
+    on bf16 MFMA.  f1 matches the numpy restatement of the bf16 arithmetic (accumulation order
+    aside: 2e-3 absolute), stays close to the fp32 parity value (0.05 absolute on these rows),
+    f2/f3 are unchanged, and an attack in bf16 mode reports the bf16 f1 of its final genes."""
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, DenseMLPModel
+    from moeva2_amd.io.tf_bundle import DenseMLP
+    from moeva2_amd.problem import get_engine
+
+    p = Project("botnet")
+    if wide:
+        W, bs = _wide_mlp()
+        clf = Classifier(DenseMLPModel(DenseMLP(W, bs, ["relu"] * 3 + ["softmax"])))
+    else:
+        clf = make_classifier("botnet")
+        dw = clf.dense_weights()
+        W, bs = [np.asarray(w, np.float32) for w in dw.weights], [np.asarray(b, np.float32) for b in dw.biases]
+    c, sc = make_constraints("botnet"), make_scaler("botnet")
+    X = p.x[:5]
+    eng = get_engine(c, clf, sc, 2)
+    mut = np.asarray(eng.prog.mut_feats)
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    rng = np.random.default_rng(11)
+    n = 70
+    genes = np.empty((X.shape[0], n, p.lay.V))
+    for b in range(X.shape[0]):
+        prob = p.problem(X[b])
+        gl, gu = mo.genetic_bounds(p.lay, prob.xl, prob.xu)
+        g = np.repeat(mo.initial_population(prob, 1), n, axis=0)
+        k = rng.integers(0, p.lay.V, size=(n, 4))
+        for r in range(n):
+            g[r, k[r]] = np.round(rng.uniform(gl[k[r]], gu[k[r]]))
+        genes[b] = g
+    gd = torch.as_tensor(genes, device="cuda")
+    F32 = torch.empty((X.shape[0], n, 3), dtype=torch.float64, device="cuda")
+    F16 = torch.empty_like(F32)
+    try:
+        eng.set_mlp_precision("fp32")
+        eng.evaluate(gd, F32)
+        eng.set_mlp_precision("bf16")
+        eng.evaluate(gd, F16)
+        torch.cuda.synchronize()
+        F32, F16 = F32.cpu().numpy(), F16.cpu().numpy()
+        np.testing.assert_array_equal(F16[:, :, 1:], F32[:, :, 1:])
+        worst = 0.0
+        for b in range(X.shape[0]):
+            x_ml = mo.genetic_to_ml(p.lay, genes[b], X[b]) * p.ml[0] + p.ml[1]
+            emu = _bf16_forward(x_ml, mut, W, bs)[:, 1]
+            np.testing.assert_allclose(F16[b, :, 0], emu, rtol=0, atol=2e-3)
+            worst = max(worst, float(np.abs(F16[b, :, 0] - F32[b, :, 0]).max()))
+        print(f"bf16 vs fp32 f1: max |diff| {worst:.2e}")
+        assert worst < 0.05
+        from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
+
+        ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_iter=200)
+        eng.attack_run(5, 23, 10, 3, ref_dirs, 0.05, 0)
+        g = torch.empty((X.shape[0], 23, p.lay.V), dtype=torch.float64, device="cuda")
+        Fa = torch.empty((X.shape[0], 23, 3), dtype=torch.float64, device="cuda")
+        eng.attack_population(g, Fa)
+        torch.cuda.synchronize()
+        g, Fa = g.cpu().numpy(), Fa.cpu().numpy()
+        assert np.isfinite(Fa).all()
+        for b in range(X.shape[0]):
+            x_ml = mo.genetic_to_ml(p.lay, g[b], X[b]) * p.ml[0] + p.ml[1]
+            np.testing.assert_allclose(Fa[b, :, 0], _bf16_forward(x_ml, mut, W, bs)[:, 1],
+                                       rtol=0, atol=2e-3)
+    finally:
+        eng.set_mlp_precision("fp32")
+
+
 # ------------------------------------------------------------------ survival
 def _random_F(rng, B, N):
     F = np.empty((B, N, 3))
