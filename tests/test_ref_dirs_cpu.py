@@ -1,0 +1,70 @@
+"""The engine's shipped energy reference directions (resources/ref_dirs/, used for
+get_reference_directions("energy", 3, n_pop, seed=1) at
+/root/reference/src/attacks/moeva2/moeva2.py:113) against the properties of pymoo's Riesz
+s-energy method, restated in oracle/ref_dirs_pymoo.py.  pymoo is not vendored, so the point
+set itself is parity-unpinned; these tests pin the method's measurable outcomes: points on
+the simplex, the corners kept, a Riesz energy (d = 2 n_dim) within 2 % of the restated
+method's optimum and well below its starting point and uniform random points, and the
+spacing / covering radius of a uniform design."""
+import numpy as np
+import pytest
+
+from oracle import ref_dirs_pymoo as rp
+
+
+def _min_dist(X):
+    d = np.sqrt(((X[:, None] - X[None]) ** 2).sum(-1))
+    np.fill_diagonal(d, np.inf)
+    return d.min()
+
+
+def _cover_radius(X, rng, n=5000):
+    P = rng.dirichlet(np.ones(X.shape[1]), size=n)
+    best = np.full(n, np.inf)
+    for s in range(0, len(X), 64):
+        best = np.minimum(best, ((P[:, None, :] - X[None, s:s + 64]) ** 2).sum(-1).min(1))
+    return float(np.sqrt(best.max()))
+
+
+@pytest.fixture(scope="module")
+def restated():
+    # iteration caps keep the CPU suite short; the restated runs are then slightly above the
+    # method's converged energy, which only loosens the 2 % comparison towards the shipped set
+    return {n: rp.energy_dirs(3, n, seed=1, n_max_iter=120 if n > 300 else 400)
+            for n in (200, 640)}
+
+
+@pytest.mark.parametrize("n", [200, 640])
+def test_shipped_dirs_vs_riesz_energy_method(restated, n):
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    X = energy_ref_dirs(3, n, seed=1)
+    R = restated[n]
+    rng = np.random.default_rng(3)
+    d = 6.0  # pymoo: d = 2 * n_dim
+    e_ship = rp.riesz_log_energy(X, d)
+    e_meth = rp.riesz_log_energy(R, d)
+    e_init = rp.riesz_log_energy(rp.reduction_init(3, n, np.random.default_rng(1)), d)
+    e_rand = rp.riesz_log_energy(rng.dirichlet(np.ones(3), size=n), d)
+    print(f"n={n}: log energy shipped {e_ship:.3f} method {e_meth:.3f} init {e_init:.3f} "
+          f"random {e_rand:.3f}")
+    # on the simplex, corners present (the extreme directions)
+    np.testing.assert_allclose(X.sum(1), 1.0, atol=1e-12)
+    assert X.min() >= 0.0
+    for k in range(3):
+        assert np.isclose(X, np.eye(3)[k], atol=1e-9).all(1).any()
+    # the method's optimum: the restated run lowers the reduction start, the shipped set sits
+    # within 2 % of it (log energies are ~ 6 log(1/spacing) large), far below random points
+    assert e_meth < e_init
+    assert abs(e_ship - e_meth) <= 0.02 * abs(e_meth)
+    assert e_ship < e_rand - 5.0
+    # uniform design: spacing and covering radius comparable to the restated method's
+    assert _min_dist(X) >= 0.6 * _min_dist(R)
+    assert _cover_radius(X, rng) <= 1.5 * _cover_radius(R, rng)
+
+
+def test_restated_method_steps_stay_on_simplex():
+    X = rp.energy_dirs(3, 24, seed=2, n_max_iter=50)
+    np.testing.assert_allclose(X.sum(1), 1.0, atol=1e-12)
+    assert X.min() >= 0.0
+    assert _min_dist(X) > 0.05
