@@ -922,6 +922,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     HIPCHK(stage_rows(vq[q], gs[q], &slot_va[q]));
   }
   sa.N = P + O;
+  const bool rows_fused = std::getenv("MV_ROWS_FUSED") && e->cx_kind == 0 &&
+                          rows_fused_lds(e->p) <= 160 * 1024;
   for (int g = 1; g < G; ++g) {
     const int hist_row0 = P + (g - 1) * O;
     sa.gen = g;
@@ -931,9 +933,14 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       hipStream_t st = gs[q];
       const bool prof = e->profiling && q == 0;
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
-      HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
-      HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
+      if (rows_fused) {  // development A/B: k_gen + k_cons as one k_rows launch
+        HIPCHK(launch_rows_fused(vq[q], slot_va[q], g, hist_row0, st));
+        if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+      } else {
+        HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
+        if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+        HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
+      }
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
       HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));

@@ -273,29 +273,8 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
   } else if (mine) {
     par_v = irow | (irow << 16);
   }
-  // Parent genes of row k: 32-bit element offsets from the state's pool (S * V < 2^31) with
-  // the two parents' row offsets wave-uniform, so each gene costs a select and an add (64-bit
-  // pointer arithmetic per gene was about a third of the row loop's VALU).
   auto load_row = [&](int k, double* x) {
-    int Vo = V;
-    asm volatile("" : "+s"(Vo));  // keep the per-t bounds out of loop-invariant hoisting
-    const int pr = rdl(par_v, k);
-    const int cx0 = rdl(cx0_v, k), cx1 = rdl(cx1_v, k);
-    const unsigned own = (unsigned)(pr & 0xFFFF) * (unsigned)Vo;
-    const unsigned oth = (unsigned)(pr >> 16) * (unsigned)Vo;
-    // swapped_packed, branch-free: the segment [lo, lo + n) of each subset (n = 0 when the
-    // subset's crossover is off) as wave-uniform scalars, one unsigned compare per gene
-    const int lo0 = (cx0 >> 1) & 0x7FFF, lo1 = (cx1 >> 1) & 0x7FFF;
-    const unsigned n0 = (cx0 & 1) ? (unsigned)((cx0 >> 16) - lo0) : 0u;
-    const unsigned n1 = (cx1 & 1) ? (unsigned)((cx1 >> 16) - lo1) : 0u;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int g = lane + 64 * t;
-      const unsigned gc = (unsigned)(g < Vo ? g : Vo - 1);
-      const bool real = (ginf[t] & 3) == 0;
-      const unsigned d = (unsigned)(((ginf[t] >> 2) & 0x7FFF) - (real ? lo0 : lo1));
-      x[t] = gin[(d < (real ? n0 : n1) ? oth : own) + gc];
-    }
+    load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x);
   };
   const bool l2 = p.norm == 2;
   // child genes -> pool, fp32 ML row, f2 (row k of this wave, genes already mutated)
@@ -371,21 +350,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
                   rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen, a.sbx_eta, lane);
       mutate_row_full<NT>(x, s_geo, s_ginfo, sgl, sgu, V, i, rng, gen, a.eta, lane);
     } else if (a.mode == 1) {  // apply the row's cached mutations
-      const int nmut = rdl(mut_v, k) & 7;
-#pragma unroll
-      for (int q = 0; q < MUT_CAP; ++q) {
-        if (q < nmut) {
-          // the position is wave-uniform: its register index t = pos / 64 is a scalar
-          // branch, and only that register is updated (on lane pos % 64)
-          const int pos = rdl(mpos[q], k);
-          const double y = rdl_d(mval[q], k);
-          const int tt = pos >> 6;
-          const bool me = lane == (pos & 63);
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            if (t == tt) x[t] = me ? y : x[t];
-        }
-      }
+      apply_row_mutations<NT>(x, rdl(mut_v, k) & 7, mpos, mval, k, lane);
     }
     finish_row(k, x);
   }

@@ -169,6 +169,10 @@ hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream);
 hipError_t launch_rows(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream);
+// k_rows: k_gen + k_cons fused (rows_fused.h); rows_fused_lds: its LDS bytes
+hipError_t launch_rows_fused(const RowsArgs& a, int slot, int gen, int hist_row0,
+                             hipStream_t stream);
+size_t rows_fused_lds(const DProblem& p);
 hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double* x,
                               double* G, hipStream_t stream);
 hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,

@@ -152,7 +152,7 @@ __device__ __forceinline__ double constraints_row(const OpTab& t, const double* 
 // packed in registers -- code (4 bits) | a0 (14) | a1 (14) -- so a row's operand reads are
 // independent LDS loads issued back to back.  DIFF and RATIO_SAFE (the botnet program) are
 // evaluated inline; other codes, and ops beyond OPS_REG per lane, go through eval_op.
-constexpr int OPS_REG = 8;
+constexpr int OPS_REG = 6;
 
 __device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
   const int4 ar = t.arg[c];
@@ -582,6 +582,53 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
     for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) af[rt] = an[rt];
+  }
+}
+
+// Parent genes of one child row (k_gen, k_rows / the whole-attack row phase): lane l loads
+// genes l + 64 t from the own or the other parent.  32-bit element offsets from the state's
+// pool (S * V < 2^31) with the two parents' row offsets wave-uniform, and swapped_packed in
+// branch-free form: the segment [lo, lo + n) of each subset (n = 0 when the subset's
+// crossover is off) as scalars, one unsigned compare per gene.  (64-bit pointer arithmetic
+// and the branchy test per gene were about a third of k_gen's row-loop VALU.)
+template <int NT>
+__device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, int V, int pr,
+                                                int cx0, int cx1, const int (&ginf)[NT],
+                                                int lane, double* x) {
+  int Vo = V;
+  asm volatile("" : "+s"(Vo));  // keep the per-t bounds out of loop-invariant hoisting
+  const unsigned own = (unsigned)(pr & 0xFFFF) * (unsigned)Vo;
+  const unsigned oth = (unsigned)(pr >> 16) * (unsigned)Vo;
+  const int lo0 = (cx0 >> 1) & 0x7FFF, lo1 = (cx1 >> 1) & 0x7FFF;
+  const unsigned n0 = (cx0 & 1) ? (unsigned)((cx0 >> 16) - lo0) : 0u;
+  const unsigned n1 = (cx1 & 1) ? (unsigned)((cx1 >> 16) - lo1) : 0u;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int g = lane + 64 * t;
+    const unsigned gc = (unsigned)(g < Vo ? g : Vo - 1);
+    const bool real = (ginf[t] & 3) == 0;
+    const unsigned d = (unsigned)(((ginf[t] >> 2) & 0x7FFF) - (real ? lo0 : lo1));
+    x[t] = gin[(d < (real ? n0 : n1) ? oth : own) + gc];
+  }
+}
+
+// The cached mutations of row k (positions / values held by lane k): each position is
+// wave-uniform, so its register index t = pos / 64 is a scalar branch and only that
+// register is updated, on lane pos % 64.
+template <int NT, int CAP>
+__device__ __forceinline__ void apply_row_mutations(double* x, int nmut, const int (&mpos)[CAP],
+                                                    const double (&mval)[CAP], int k, int lane) {
+#pragma unroll
+  for (int q = 0; q < CAP; ++q) {
+    if (q < nmut) {
+      const int pos = rdl(mpos[q], k);
+      const double y = rdl_d(mval[q], k);
+      const int tt = pos >> 6;
+      const bool me = lane == (pos & 63);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t == tt) x[t] = me ? y : x[t];
+    }
   }
 }
 

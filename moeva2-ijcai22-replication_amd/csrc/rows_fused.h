@@ -184,17 +184,7 @@ __device__ __forceinline__ void rows_state(const RowsArgs& a, const int b, const
       par_v = irow | (irow << 16);
     }
     auto load_row = [&](int k, double* x) {
-      int Vo = V;
-      asm volatile("" : "+s"(Vo));
-      const int pr = rdl(par_v, k);
-      const int cx0 = rdl(cx0_v, k), cx1 = rdl(cx1_v, k);
-      const double* gown = gin + (size_t)(pr & 0xFFFF) * V;
-      const double* goth = gin + (size_t)(pr >> 16) * V;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int g = lane + 64 * t;
-        x[t] = (swapped_packed(ginf[t], cx0, cx1) ? goth : gown)[g < Vo ? g : Vo - 1];
-      }
+      load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x);
     };
     // child genes -> pool, fp32 ML row, f2, constraint program -> f3 (row k of this wave)
     auto finish_row = [&](int k, const double* x) {
@@ -283,17 +273,7 @@ __device__ __forceinline__ void rows_state(const RowsArgs& a, const int b, const
                     rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen, a.sbx_eta, lane);
         mutate_row_full<NT>(x, s_geo, s_ginfo, sgl, sgu, V, i, rng, gen, a.eta, lane);
       } else if (a.mode == 1) {
-        const int nmut = rdl(mut_v, k) & 7;
-#pragma unroll
-        for (int q = 0; q < MUT_CAP; ++q) {
-          if (q < nmut) {
-            const int pos = rdl(mpos[q], k);
-            const double y = rdl_d(mval[q], k);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-              if (pos == lane + 64 * t) x[t] = y;
-          }
-        }
+        apply_row_mutations<NT>(x, rdl(mut_v, k) & 7, mpos, mval, k, lane);
       }
       finish_row(k, x);
     }
