@@ -648,6 +648,38 @@ def test_moeva2_generate_api_lcld():
     assert res[0].X.shape[1] == 15 and res[0].F.shape[1] == 3
 
 
+def test_generate_sharded_real_engine_world1():
+    """Moeva2.generate_sharded with the real engine on a one-rank RCCL group (the multi-GPU
+    path's padding + all_gather around Moeva2.generate(return_device=True)): the gathered
+    populations equal an unsharded generate of the same states and seed."""
+    import socket
+
+    import torch.distributed as dist
+
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+
+    c = make_constraints("lcld")
+    p = Project("lcld")
+    m = Moeva2(os.path.join(RES, PROJECTS["lcld"][1]), c, ml_scaler=make_scaler("lcld"), norm=2,
+               n_gen=5, n_pop=40, n_offsprings=20, seed=11)
+    X = p.x[:5]
+    g0, F0, _ = m.generate(X, 1, return_device=True)
+    g0, F0 = g0.cpu().numpy(), F0.cpu().numpy()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        g1, F1 = m.generate_sharded(X, 1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(g1.cpu().numpy(), g0)
+        np.testing.assert_array_equal(F1.cpu().numpy(), F0)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_success_rate_matches_oracle_attack():
     """End to end (north_star): the constrained success rates o1..o7
     (objective_calculator.py:86-119) of the device attack against the oracle's CPU attack
