@@ -384,6 +384,22 @@ def main():
                              surv_bytes_state * B, surv_ms, "k_survive"),
         }
         per_gen = {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+        # LCLD-shaped rows run k_narrow (csrc/narrow.h narrow_ok): variation + decode + f2 +
+        # constraint program in ONE launch timed as "k_gen"; the "k_cons" events then bracket
+        # an empty step, so the pair is reported as one kernel with the combined bytes
+        # (parents read + child written + ML row + f2/f3 + history columns per row)
+        prog = eng.prog
+        narrow = (V <= 32 and Dm4 <= 64 and prog.C <= 64 and not (prog.op_code == 3).any()
+                  and args.crossover == "two_point" and os.environ.get("MV_NARROW") != "0")
+        if narrow:
+            hist_b = {"full": 8 * (3 + prog.C), "reduced": 24}.get(w["history"], 0)
+            nb = 2 * V * 8 + Dm4 * 4 + 16 + hist_b
+            kernels.pop("k_gen")
+            kernels.pop("k_cons")
+            kernels["k_narrow"] = hbm("k_narrow (crossover + mutation + ML row + distance + "
+                                      "constraint program, one lane per row)", nb * rows,
+                                      gen_ms + cons_ms, "k_gen")
+            per_gen = {"k_narrow": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
         per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
     dom = per_gen["dominant"]
     if args.shard:

@@ -930,6 +930,207 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_mlpw: the bf16 perf mode for WIDE hidden layers (BASELINE configs[4]: 756-512-512-256-2,
+// widths up to 512) -- 64-row persistent tiles, 8 waves.  Activations live in LDS as bf16
+// (two [64][hs] ping-pong buffers, 133 KiB at width 512; fp32 tiles of 64 rows would not
+// fit, which is why fp32 keeps k_mlp's 32-row tiles), so each weight byte streamed from L2
+// serves 64 rows instead of 32.  Per k-step of 32 a wave issues 4 ds_read_b128 (its A
+// fragments: lane (il, ka) holds row il, k = 32 s + 8 ka + j), CJ dwordx4 weight loads (the
+// next step's prefetched) and 4 CJ v_mfma_f32_16x16x32_bf16.  The last hidden layer's
+// outputs stay fp32 in registers and fold straight into the final Dense (partial sums over
+// each lane's columns, a 16-lane butterfly, then the 8 waves' parts in order) -> softmax ->
+// f1.  Arithmetic = the k_mlp2 bf16 mode's (inputs of every hidden layer rounded to bf16).
+constexpr int MW_ROWS = 64;
+constexpr int MW_T = 512;
+struct MwLds {
+  unsigned h0, h1, part, total;
+  int hs;  // bf16 row stride of the activation buffers
+};
+__host__ __device__ inline MwLds mlpw_lds(const DProblem& p) {
+  const int nl = p.n_layers;
+  int w = (p.Dm4 + 31) & ~31;
+  for (int l = 1; l < nl; ++l) w = p.dims[l] > w ? p.dims[l] : w;
+  MwLds L{};
+  L.hs = w + 8;  // 16-B row padding: consecutive rows start 4 banks apart
+  const unsigned head =
+      256 + (((unsigned)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~15u);
+  const unsigned hb = (unsigned)MW_ROWS * L.hs * 2;
+  L.h0 = head;
+  L.h1 = L.h0 + hb;
+  L.part = L.h1 + hb;
+  L.total = L.part + (unsigned)(MW_T / 64) * MW_ROWS * p.dims[nl] * 4;
+  return L;
+}
+
+template <int CJ>
+__global__ __launch_bounds__(MW_T) void k_mlpw(int slot, int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int il = lane & 15, ka = lane >> 4;
+  const int nl = p.n_layers;
+  const int K0 = p.Dm4;
+  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
+  const MwLds L = mlpw_lds(p);
+  const int hs = L.hs;
+  int* rowst = (int*)smem;
+  float* wl = (float*)(smem + 256);
+  float* bl = wl + Klast * nout;
+  __bf16* H0 = (__bf16*)(smem + L.h0);
+  __bf16* H1 = (__bf16*)(smem + L.h1);
+  float* part = (float*)(smem + L.part);
+  for (int q = tid; q < Klast * nout; q += MW_T) wl[q] = p.W[nl - 1][q];
+  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
+  const int nq = ((K0 + 31) & ~31) >> 3;  // 8-k groups of the layer-0 tile (K zero padded)
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r0 = tile * MW_ROWS;
+    __syncthreads();  // the previous tile's readers of rowst / H / part are done
+    if (tid < MW_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
+    // layer-0 input: the fp32 ML rows rounded to bf16
+    for (int idx = tid; idx < MW_ROWS * nq; idx += MW_T) {
+      const int row = idx / nq, q = idx - row * nq;
+      const int k = 8 * q;
+      const int rr = r0 + row < a.total ? r0 + row : a.total - 1;
+      const bool on = k < K0;
+      const float* src = a.xml + (size_t)rr * K0 + (on ? k : 0);
+      *(bf16x8*)(H0 + row * hs + k) = to_bf16x8(*(const float4*)src, *(const float4*)(src + 4), on);
+    }
+    __syncthreads();
+    for (int l = 0; l + 1 < nl; ++l) {
+      const __bf16* in = (l & 1) ? H1 : H0;
+      __bf16* out = (l & 1) ? H0 : H1;
+      const int K = l == 0 ? K0 : p.dims[l];
+      const int N = p.dims[l + 1];
+      const int nct = N >> 4;
+      const int nst = (K + 31) >> 5;
+      const __bf16* W = (const __bf16*)p.Wb[l];
+      floatx4 acc[CJ][4];
+#pragma unroll
+      for (int j = 0; j < CJ; ++j)
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) acc[j][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      auto load_b = [&](int st, bf16x8 (&bf)[CJ]) {
+        const int sc = st < nst ? st : nst - 1;
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+          const int ct = wave + 8 * j < nct ? wave + 8 * j : nct - 1;
+          bf[j] = *(const bf16x8*)(W + ((size_t)sc * N + ct * 16 + il) * 32 + 8 * ka);
+        }
+      };
+      bf16x8 bf[CJ];
+      load_b(0, bf);
+      for (int st = 0; st < nst; ++st) {
+        bf16x8 bn[CJ];
+        load_b(st + 1, bn);
+        const int k = 32 * st + 8 * ka;
+        bf16x8 af[4];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          af[rt] = *(const bf16x8*)(in + (rt * 16 + il) * hs + (k < K ? k : 0));
+          if (k >= K) af[rt] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+          if (wave + 8 * j < nct) {
+#pragma unroll
+            for (int rt = 0; rt < 4; ++rt)
+              acc[j][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bf[j], acc[j][rt], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) bf[j] = bn[j];
+      }
+      const bool last = l + 2 == nl;
+      // + bias, ReLU in place; hidden outputs to LDS as bf16
+#pragma unroll
+      for (int j = 0; j < CJ; ++j) {
+        const int ct = wave + 8 * j;
+        if (ct < nct) {
+          const int col = ct * 16 + il;
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int row = rt * 16 + ka * 4 + jj;
+              float bv;
+              if (l == 0) {
+                const int s = rowst[row];
+                bv = a.s.bias1[(size_t)(s < 0 ? 0 : s) * N + col];
+              } else {
+                bv = p.bias[l][col];
+              }
+              const float v = acc[j][rt][jj] + bv;
+              acc[j][rt][jj] = v > 0.f ? v : 0.f;
+              if (!last) out[row * hs + col] = (__bf16)acc[j][rt][jj];
+            }
+          }
+        }
+      }
+      if (last) {
+        // the final Dense from the fp32 registers: per class, partial logits over this lane's
+        // columns, summed over the 16 lanes sharing the rows, one part per wave
+        for (int c = 0; c < nout; ++c) {
+          float ps[4][4];
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) ps[rt][jj] = 0.f;
+#pragma unroll
+          for (int j = 0; j < CJ; ++j) {
+            const int ct = wave + 8 * j;
+            if (ct < nct) {
+              const float wv = wl[(ct * 16 + il) * nout + c];
+#pragma unroll
+              for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) ps[rt][jj] = fmaf(acc[j][rt][jj], wv, ps[rt][jj]);
+            }
+          }
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              float v = ps[rt][jj];
+              v += __shfl_xor(v, 1);
+              v += __shfl_xor(v, 2);
+              v += __shfl_xor(v, 4);
+              v += __shfl_xor(v, 8);
+              if (il == 0) part[(wave * MW_ROWS + rt * 16 + ka * 4 + jj) * nout + c] = v;
+            }
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < MW_ROWS) {
+      const int s = rowst[tid];
+      if (s >= 0) {
+        double z[8];
+        double mx = -__builtin_inf();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          z[c] = 0.0;
+          if (c < nout) {
+            float t = 0.f;
+            for (int w = 0; w < MW_T / 64; ++w) t += part[(w * MW_ROWS + tid) * nout + c];
+            z[c] = (double)(t + bl[c]);
+            mx = z[c] > mx ? z[c] : mx;
+          }
+        }
+        const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
+        const int i = r0 + tid - s * a.n;
+        if (a.F) {
+          const int orow = a.out_map ? a.out_map[(size_t)s * a.n + i] : i;
+          a.F[((size_t)s * a.out_rows + orow) * 3] = f1;
+        }
+        if (a.hist) a.hist[((size_t)s * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
+      }
+    }
+  }
+}
+
 // Classifier.predict_proba: 16 RT rows per workgroup, full-width first layer.
 template <int MAXCT, int RT = 2>
 __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
@@ -1369,6 +1570,20 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   return hipGetLastError();
 }
 
+template <int CJ>
+static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_mlpw<CJ>);
+    configured = true;
+  }
+  const size_t lds = mlpw_lds(a.p).total;
+  const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
+  const int grid = ntiles < cu_count() ? ntiles : cu_count();  // one 133-KiB workgroup per CU
+  hipLaunchKernelGGL((k_mlpw<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
+  return hipGetLastError();
+}
+
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
   if (a.p.mlp2 && !std::getenv("MV_MLP_V1")) {
@@ -1377,6 +1592,12 @@ hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t st
                                   : mlp2_go<2, true>(a, slot, hist_row0, stream);
     return mlp2_hmax(a.p) <= 64 ? mlp2_go<1, false>(a, slot, hist_row0, stream)
                                 : mlp2_go<2, false>(a, slot, hist_row0, stream);
+  }
+  if (a.p.mlp_bf16 && mlpw_lds(a.p).total <= 160 * 1024 && !std::getenv("MV_MLPW_OFF")) {
+    const int hm = max_hidden(a.p.dims, a.p.n_layers);
+    return hm <= 128 ? mlpw_go<1>(a, slot, hist_row0, stream)
+                     : hm <= 256 ? mlpw_go<2>(a, slot, hist_row0, stream)
+                                 : mlpw_go<4>(a, slot, hist_row0, stream);
   }
   configure_lds_once();
   const int nl = a.p.n_layers;
