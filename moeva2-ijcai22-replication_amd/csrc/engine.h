@@ -78,6 +78,10 @@ struct DProblem {
   // accumulation, final Dense + softmax unchanged
   const unsigned short* Wb[MAX_LAYERS];
   int mlp_bf16;
+  // k_mlp2 builds its layer-0 tiles straight from the child genes (IDENT problems: gene g
+  // is mutable feature g), so k_gen writes no fp32 ML row: the xml hand-off (Dm4 * 4 B
+  // written + read back per row) is gone
+  int xml_direct;
 };
 
 struct DStates {

@@ -293,6 +293,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
     float* xo = a.xml + ((size_t)b * a.n + i) * Dm4;
     double acc = 0.0;
     if (IDENT) {  // gene g <-> mutable feature g: no decoding
+      const bool wx = !p.xml_direct;  // else k_mlp2 scales the child genes itself
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int j = lane + 64 * t;
@@ -300,14 +301,16 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
           float v = 0.f;
           if (j < Dmo) {
             const double xf = x[t];
-            const double ms = REGC ? cS[t] : s_mlS[j], mm = REGC ? cM[t] : s_mlM[j];
             const double es = REGC ? cE[t] : s_es[j], em = REGC ? cN[t] : s_em[j];
             const double x0 = REGC ? cX[t] : s_x0[j];
-            v = (float)(xf * ms + mm);
+            if (wx) {
+              const double ms = REGC ? cS[t] : s_mlS[j], mm = REGC ? cM[t] : s_mlM[j];
+              v = (float)(xf * ms + mm);
+            }
             const double d = (xf * es + em) - x0;
             acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
           }
-          xo[j] = v;
+          if (wx) xo[j] = v;
         }
       }
     } else {  // decode through the row buffer (feature_encoder.py:91-124)
@@ -768,6 +771,7 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
   const int il = lane & 15, ka = lane >> 4;
   const int nl = p.n_layers;
   const int K0 = p.Dm4, N0 = p.dims[1];
+  const int K0dm = p.Dm;  // genes per row (= mutable features) on the xml_direct path
   const int hld = mlp2_hmax(p) + 4;
   const int Klast = p.dims[nl - 1], nout = p.dims[nl];
   int* rowst = (int*)smem;
@@ -786,6 +790,21 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     // address-taken and lived in scratch (64 B per lane per chunk, 41 MiB of WRITE_SIZE per
     // launch in the r01 PMC pass)
     float4 st0, st1, st2, st3;
+    // xml_direct: the source rows are the tile's child genes (fp64) in the pool, ML-scaled
+    // here exactly as k_gen would have, (float)(x * mlS + mlM); row u of this thread:
+    // tile row (tid >> 4) + 16 u
+    const double* grow[4];
+    if (p.xml_direct) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rr0 = r0 + (tid >> 4) + 16 * u;
+        const int rr = rr0 < a.total ? rr0 : a.total - 1;
+        const int st = rr / a.n, i = rr - st * a.n;
+        grow[u] = a.mode == 1
+            ? a.genes_out + ((size_t)st * a.out_rows + (a.out_map ? a.out_map[rr] : i)) * K0dm
+            : a.genes_in + ((size_t)st * a.in_rows + i) * K0dm;
+      }
+    }
 #define M2_CHUNK_LOAD(c)                                                                 \
   {                                                                                      \
     const int cc = (c);                                                                  \
@@ -794,8 +813,32 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
       const int idx = tid + 256 * u;                                                     \
       const int row = idx >> 4, q = idx & 15;                                            \
       const int k = cc * 64 + 4 * q < K0 ? cc * 64 + 4 * q : K0 - 4;                     \
-      const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                        \
-      *sts[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);                           \
+      if (p.xml_direct) {                                                                \
+        float v4[4];                                                                     \
+        if (k + 3 < K0dm) {  /* four genes: two 16-B loads (+ the scaler's) */           \
+          const double2 g01 = *(const double2*)(grow[u] + k);                           \
+          const double2 g23 = *(const double2*)(grow[u] + k + 2);                       \
+          const double2 s01 = *(const double2*)(p.mlS + k);                             \
+          const double2 s23 = *(const double2*)(p.mlS + k + 2);                         \
+          const double2 m01 = *(const double2*)(p.mlM + k);                             \
+          const double2 m23 = *(const double2*)(p.mlM + k + 2);                         \
+          v4[0] = (float)(g01.x * s01.x + m01.x);                                        \
+          v4[1] = (float)(g01.y * s01.y + m01.y);                                        \
+          v4[2] = (float)(g23.x * s23.x + m23.x);                                        \
+          v4[3] = (float)(g23.y * s23.y + m23.y);                                        \
+        } else {                                                                         \
+          _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                \
+            const int kk = k + e;                                                        \
+            const int kc = kk < K0dm ? kk : K0dm - 1;                                    \
+            const float v = (float)(grow[u][kc] * p.mlS[kc] + p.mlM[kc]);                \
+            v4[e] = kk < K0dm ? v : 0.f;                                                 \
+          }                                                                              \
+        }                                                                                \
+        *sts[u] = make_float4(v4[0], v4[1], v4[2], v4[3]);                               \
+      } else {                                                                           \
+        const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                      \
+        *sts[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);                         \
+      }                                                                                  \
     }                                                                                    \
   }
 #define M2_CHUNK_STORE(buf)                                                              \
@@ -1586,7 +1629,8 @@ static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
-  if (a.p.mlp2 && !std::getenv("MV_MLP_V1")) {
+  // (MV_MLPW=1: the bf16 mode runs k_mlpw for narrow nets too -- development A/B)
+  if (a.p.mlp2 && !std::getenv("MV_MLP_V1") && !(a.p.mlp_bf16 && std::getenv("MV_MLPW"))) {
     if (a.p.mlp_bf16)
       return mlp2_hmax(a.p) <= 64 ? mlp2_go<1, true>(a, slot, hist_row0, stream)
                                   : mlp2_go<2, true>(a, slot, hist_row0, stream);
