@@ -336,7 +336,15 @@ def main():
     #   k_gen : parent genes read + child genes written (2*V*8) + fp32 ML row (Dm4*4) + f2 (8)
     #   k_cons: child genes read (V*8) + f3 (8)
     #   k_survive: merged F read (N*3*8) + survivor/free slots + parents (4*(P+O+O)) per state
-    gen_bytes = 2 * V * 8 + Dm4 * 4 + 8
+    # xml_direct (csrc/engine.h: IDENT problems with a k_mlp2 classifier, the botnet shape):
+    # k_gen writes no fp32 ML row, k_mlp2 reads the child genes itself
+    prog = eng.prog
+    ident = (V == Dm and int((prog.gene_kind == 2).sum()) == 0
+             and np.array_equal(prog.gene_feat, prog.mut_feats))
+    hidden = dims_full[1:-1]
+    xml_direct = (ident and all(h % 16 == 0 and h <= 128 for h in hidden)
+                  and "MV_XML" not in os.environ)
+    gen_bytes = 2 * V * 8 + (0 if xml_direct else Dm4 * 4) + 8
     cons_bytes = V * 8 + 8
     surv_bytes_state = (P + O) * 3 * 8 + 4 * (P + 2 * O)
 
@@ -388,7 +396,6 @@ def main():
         # constraint program in ONE launch timed as "k_gen"; the "k_cons" events then bracket
         # an empty step, so the pair is reported as one kernel with the combined bytes
         # (parents read + child written + ML row + f2/f3 + history columns per row)
-        prog = eng.prog
         narrow = (V <= 32 and Dm4 <= 64 and prog.C <= 64 and not (prog.op_code == 3).any()
                   and args.crossover == "two_point" and os.environ.get("MV_NARROW") != "0")
         if narrow:

@@ -913,6 +913,12 @@ def test_objective_calculator_range_assert():
     xs[1, 2, j] = (2.0 - mn[j]) / sc[j]  # scales to 2.0
     with pytest.raises(AssertionError):
         calc.calculate_objectives_3d(X, xs)
+    # a NaN candidate fails the same np.all range asserts in the reference (NaN comparisons
+    # are False), so it is never scored as a successful attack
+    xs = np.repeat(X[:, None], 3, axis=1).copy()
+    xs[0, 1, 0] = np.nan
+    with pytest.raises(AssertionError):
+        calc.calculate_objectives_3d(X, xs)
 
 
 def test_moeva_driver_outputs(tmp_path):
