@@ -18,7 +18,19 @@ namespace mv {
 constexpr int MAX_LAYERS = 6;
 constexpr int EVAL_TR = 32;      // rows per evaluation tile (two 16-row MFMA tiles)
 constexpr int EVAL_T = 256;      // threads per evaluation workgroup (4 waves)
-constexpr int VARY_T = 256;      // threads per k_gen / k_cons workgroup (4 waves)
+#ifndef MV_VARY_T
+#define MV_VARY_T 256
+#endif
+constexpr int VARY_T = MV_VARY_T; // threads per k_gen / k_cons workgroup
+constexpr int VARY_W = VARY_T / 64;  // its waves: wave w takes rows w, w + VARY_W, ...
+#ifndef MV_CONS_T
+#define MV_CONS_T 256
+#endif
+// k_cons workgroup threads.  512 makes the kernel alone faster (66 -> 58 us) but the
+// four-group attack slower (152.3 -> 149.9 M evals/s, A/B on one box): the concurrent
+// schedule is bound by the chip's aggregate issue/latency capacity, not one kernel's.
+constexpr int CONS_T = MV_CONS_T;
+constexpr int CONS_W = CONS_T / 64;
 constexpr int VARY_ROWS_MAX = 32; // rows of one state per k_gen / k_cons workgroup (swept: 16/32/64)
 constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)

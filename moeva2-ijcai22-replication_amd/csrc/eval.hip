@@ -189,7 +189,7 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
 // SBX: the SBX crossover option compiled in (a separate instance: its pow()-heavy path
 // doubled the two-point kernel's registers, halving its occupancy).
 template <bool IDENT, int NT, bool SBX>
-__global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
+__global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
   const double* sgu = a.s.gu + (size_t)b * V;
   const bool sbx = SBX && a.mode == 1;
   const bool mine = lane < nrw;
-  const int irow = rc.i0 + wave + 4 * lane;
+  const int irow = rc.i0 + wave + VARY_W * lane;
   if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
   if (a.mode == 1) {
     row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
   auto finish_row = [&](int k, const double* x) {
     int Vo = V, Dmo = Dm, Dm4o = Dm4;
     asm volatile("" : "+s"(Vo), "+s"(Dmo), "+s"(Dm4o));
-    const int i = rc.i0 + wave + 4 * k;
+    const int i = rc.i0 + wave + VARY_W * k;
     const int orow = rdl(orow_v, k);
     if (a.genes_out) {
       double* gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
     for (int t = 0; t < NT; ++t) x[t] = xn[t];
     if (k + 1 < nrw) load_row(k + 1, xn);
     if (sbx) {  // SBX children, then every mutation of the row
-      const int i = rc.i0 + wave + 4 * k;
+      const int i = rc.i0 + wave + VARY_W * k;
       const int nm = a.n / 2;
       const int pr = rdl(par_v, k);
       sbx_row<NT>(x, ginf, gin + (size_t)(pr >> 16) * V, sgl, sgu, V, i % nm, i / nm,
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
     const float lq = __log2f(1.0f - 1.0f / (float)V);
     for (int k = 0; k < nrw; ++k) {
       if (!(rdl(mut_v, k) & 8)) continue;
-      const int i = rc.i0 + wave + 4 * k;
+      const int i = rc.i0 + wave + VARY_W * k;
       double x[NT];
       load_row(k, x);
       int pos = -1;
@@ -398,17 +398,17 @@ __global__ __launch_bounds__(256) void k_gen(int slot, int gen, int hist_row0, i
 // into the wave's ML row buffer whose immutable features were written once, then each lane
 // evaluates its (register-packed) ops.
 template <bool FULL, bool IDENT, int NT>
-__global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_wg) {
+__global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int rows_wg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const RowChunk rc = row_chunk(a.n, rows_wg, wave);
+  const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
   const int b = rc.b, nrw = rc.nrw;
   const int V = p.V;
   const VaryOff o = vary_offsets(p);
-  glds_copy(smem, p.vblob, o.a_end, wave, lane);
-  glds_copy(smem + o.a_end, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
+  glds_copy<CONS_T>(smem, p.vblob, o.a_end, wave, lane);
+  glds_copy<CONS_T>(smem + o.a_end, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
   int ginf[NT];
   {
     const int* gi = (const int*)(p.vblob + o.ginfo);
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_
   // row sources: mode 1 reads the children k_gen wrote (destination rows), mode 0 the input
   int src_v = 0, dst_v = 0;
   if (lane < nrw) {
-    const int i = rc.i0 + wave + 4 * lane;
+    const int i = rc.i0 + wave + CONS_W * lane;
     dst_v = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
     src_v = a.mode == 1 ? dst_v : i;
   }
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void k_cons(int slot, int hist_row0, int rows_
 #pragma unroll
     for (int t = 0; t < NT; ++t) x[t] = xn[t];
     if (k + 1 < nrw) load_row(k + 1, xn);
-    const int i = rc.i0 + wave + 4 * k;
+    const int i = rc.i0 + wave + CONS_W * k;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (lane + 64 * t < V) {
@@ -1423,7 +1423,7 @@ static hipError_t cons_go(dim3 grid, size_t lds, hipStream_t s, int slot, int h0
     allow_lds(k_cons<FULL, IDENT, NT>);
     configured = true;
   }
-  hipLaunchKernelGGL((k_cons<FULL, IDENT, NT>), grid, dim3(VARY_T), lds, s, slot, h0, rw);
+  hipLaunchKernelGGL((k_cons<FULL, IDENT, NT>), grid, dim3(CONS_T), lds, s, slot, h0, rw);
   return hipGetLastError();
 }
 

@@ -112,7 +112,7 @@ __host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool iden
 }
 // k_cons LDS: region A, region X, one row per wave
 __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
-  return o.a_end + o.x_end + (VARY_T / 64) * o.rb;
+  return o.a_end + o.x_end + CONS_W * o.rb;
 }
 
 // fused row kernel (k_rows, whole-attack rows phase): regions A, B, C, E, then one D-wide

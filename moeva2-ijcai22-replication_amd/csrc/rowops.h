@@ -481,6 +481,7 @@ __device__ __forceinline__ int xcd_local_id() {
   const int q = G / NX, r = G % NX, x = i % NX, k = i / NX;
   return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
 }
+template <int W = VARY_W>
 __device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
   RowChunk r;
   const int nchunk = (n + rows_wg - 1) / rows_wg;
@@ -489,7 +490,7 @@ __device__ __forceinline__ RowChunk row_chunk(int n, int rows_wg, int wave) {
   r.i0 = (id - r.b * nchunk) * rows_wg;
   r.i1 = min(n, r.i0 + rows_wg);
   const int span = r.i1 - r.i0 - wave;
-  r.nrw = span > 0 ? (span + 3) / 4 : 0;
+  r.nrw = span > 0 ? (span + W - 1) / W : 0;
   return r;
 }
 
