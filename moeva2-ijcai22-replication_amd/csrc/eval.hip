@@ -762,7 +762,7 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
 // k_gen through a double-buffered LDS chunk of 64 k (register staged); hidden outputs go to
 // an LDS ping-pong; the immutable features' contribution to layer 0 is the per-state bias
 // bias1 (k_setup_states).  The last Dense + softmax is a dot product per row on the VALU.
-template <int CJ, bool BF>
+template <int CJ, bool BF, bool DIRECT>
 __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -781,6 +781,13 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
   float* H = A0;  // hidden ping-pong, aliases the layer-0 chunks
   for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
   if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  double* sS = (double*)(smem + mlp2_sc_off(p));
+  double* sM = sS + K0;
+  if (DIRECT)
+    for (int q = tid; q < K0; q += 256) {
+      sS[q] = p.mlS[q];
+      sM[q] = p.mlM[q];
+    }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
   const int nkg0 = K0 >> 4;
   const int nch = (nkg0 + 3) >> 2;
@@ -788,13 +795,16 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     const int r0 = tile * M2_ROWS;
     // the chunk staging registers are plain locals: captured by a lambda they were
     // address-taken and lived in scratch (64 B per lane per chunk, 41 MiB of WRITE_SIZE per
-    // launch in the r01 PMC pass)
+    // launch in the r01 PMC pass).  xml_direct stages the raw genes (gd) and converts them in
+    // M2_CHUNK_STORE, after the current chunk's MFMAs: converting at load time made every
+    // chunk wait for its loads before the MFMAs could hide them.
     float4 st0, st1, st2, st3;
+    double gd[DIRECT ? 4 : 1][4];
     // xml_direct: the source rows are the tile's child genes (fp64) in the pool, ML-scaled
     // here exactly as k_gen would have, (float)(x * mlS + mlM); row u of this thread:
     // tile row (tid >> 4) + 16 u
     const double* grow[4];
-    if (p.xml_direct) {
+    if (DIRECT) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int rr0 = r0 + (tid >> 4) + 16 * u;
@@ -813,47 +823,50 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
       const int idx = tid + 256 * u;                                                     \
       const int row = idx >> 4, q = idx & 15;                                            \
       const int k = cc * 64 + 4 * q < K0 ? cc * 64 + 4 * q : K0 - 4;                     \
-      if (p.xml_direct) {                                                                \
-        float v4[4];                                                                     \
-        if (k + 3 < K0dm) {  /* four genes: two 16-B loads (+ the scaler's) */           \
+      if (DIRECT) {  /* raw genes; scaled in M2_CHUNK_STORE */                   \
+        if (k + 3 < K0dm) {                                                              \
           const double2 g01 = *(const double2*)(grow[u] + k);                           \
           const double2 g23 = *(const double2*)(grow[u] + k + 2);                       \
-          const double2 s01 = *(const double2*)(p.mlS + k);                             \
-          const double2 s23 = *(const double2*)(p.mlS + k + 2);                         \
-          const double2 m01 = *(const double2*)(p.mlM + k);                             \
-          const double2 m23 = *(const double2*)(p.mlM + k + 2);                         \
-          v4[0] = (float)(g01.x * s01.x + m01.x);                                        \
-          v4[1] = (float)(g01.y * s01.y + m01.y);                                        \
-          v4[2] = (float)(g23.x * s23.x + m23.x);                                        \
-          v4[3] = (float)(g23.y * s23.y + m23.y);                                        \
+          gd[u][0] = g01.x;                                                              \
+          gd[u][1] = g01.y;                                                              \
+          gd[u][2] = g23.x;                                                              \
+          gd[u][3] = g23.y;                                                              \
         } else {                                                                         \
           _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                \
             const int kk = k + e;                                                        \
-            const int kc = kk < K0dm ? kk : K0dm - 1;                                    \
-            const float v = (float)(grow[u][kc] * p.mlS[kc] + p.mlM[kc]);                \
-            v4[e] = kk < K0dm ? v : 0.f;                                                 \
+            gd[u][e] = grow[u][kk < K0dm ? kk : K0dm - 1];                               \
           }                                                                              \
         }                                                                                \
-        *sts[u] = make_float4(v4[0], v4[1], v4[2], v4[3]);                               \
       } else {                                                                           \
         const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                      \
         *sts[u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);                         \
       }                                                                                  \
     }                                                                                    \
   }
-#define M2_CHUNK_STORE(buf)                                                              \
+#define M2_CHUNK_STORE(buf, c)                                                           \
   {                                                                                      \
     const float4 vs[4] = {st0, st1, st2, st3};                                           \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                      \
       const int idx = tid + 256 * u;                                                     \
       const int row = idx >> 4, q = idx & 15;                                            \
-      *(float4*)(A0 + (buf) * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = vs[u];           \
+      float4 v = vs[u];                                                                  \
+      if (DIRECT) {                                                                \
+        const int kq = (c) * 64 + 4 * q;                                                 \
+        const int k = kq < K0 ? kq : K0 - 4;                                             \
+        float v4[4];                                                                     \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                  \
+          const int kk = k + e;                                                          \
+          v4[e] = kk < K0dm ? (float)(gd[u][e] * sS[kk] + sM[kk]) : 0.f;                 \
+        }                                                                                \
+        v = make_float4(v4[0], v4[1], v4[2], v4[3]);                                     \
+      }                                                                                  \
+      *(float4*)(A0 + (buf) * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = v;               \
     }                                                                                    \
   }
     M2_CHUNK_LOAD(0)
     __syncthreads();  // the previous tile's readers of rowst / A0 / H are done
     if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
-    M2_CHUNK_STORE(0)
+    M2_CHUNK_STORE(0, 0)
     __syncthreads();
     floatx4 acc[CJ][4];
 #pragma unroll
@@ -870,7 +883,7 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
         mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
                        p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, tile_map(N0 >> 4, wave),
                        il, ka);
-      if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1)
+      if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1, c + 1)
       __syncthreads();
     }
 #undef M2_CHUNK_LOAD
@@ -1601,19 +1614,19 @@ static int cu_count() {
   return n;
 }
 
-template <int CJ, bool BF>
-static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+template <int CJ, bool BF, bool DIRECT>
+static hipError_t mlp2_go3(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static bool configured = false;
   static size_t occ_lds = 0;
   static int occ = 2;
   if (!configured) {
-    allow_lds(k_mlp2<CJ, BF>);
+    allow_lds(k_mlp2<CJ, BF, DIRECT>);
     configured = true;
   }
   const size_t lds = mlp2_lds(a.p);
   if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF>, 256, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF, DIRECT>, 256, lds) != hipSuccess ||
         n < 1)
       n = 1;
     (void)hipGetLastError();
@@ -1622,8 +1635,15 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
   const int grid = ntiles < occ * cu_count() ? ntiles : occ * cu_count();
-  hipLaunchKernelGGL((k_mlp2<CJ, BF>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
+  hipLaunchKernelGGL((k_mlp2<CJ, BF, DIRECT>), dim3(grid), dim3(256), lds, stream, slot,
+                     hist_row0);
   return hipGetLastError();
+}
+
+template <int CJ, bool BF>
+static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  return a.p.xml_direct ? mlp2_go3<CJ, BF, true>(a, slot, hist_row0, stream)
+                        : mlp2_go3<CJ, BF, false>(a, slot, hist_row0, stream);
 }
 
 template <int CJ>

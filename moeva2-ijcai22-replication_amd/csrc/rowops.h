@@ -519,9 +519,14 @@ __host__ __device__ inline int mlp2_region_floats(const DProblem& p) {
 __host__ __device__ inline bool mlp2_part_inplace(const DProblem& p) {
   return 4 * p.dims[p.n_layers] <= mlp2_hmax(p) + 4;
 }
-__host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
+// xml_direct: the ML scaler at the mutable features (mlS, mlM: Dm4 doubles each) staged in
+// LDS after the tile buffers
+__host__ __device__ inline size_t mlp2_sc_off(const DProblem& p) {
   return mlp2_head(p) + (size_t)mlp2_region_floats(p) * 4 +
          (mlp2_part_inplace(p) ? 0 : (size_t)4 * M2_ROWS * p.dims[p.n_layers] * 4);
+}
+__host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
+  return mlp2_sc_off(p) + (p.xml_direct ? (size_t)2 * p.Dm4 * 8 : 0);
 }
 
 // A wave's share of a layer's (column tile, row tile) grid: column tiles cb + 4cj over all
