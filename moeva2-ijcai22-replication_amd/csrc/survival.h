@@ -53,7 +53,7 @@ struct SurvLds {
   int* csr;         // [N]
   int* cand;        // [R+3]
   int* ckey;        // [R+3]
-  int* iscal;       // [16]
+  int* iscal;       // [16 + SURV_TMAX / 64]: scalars [0, 16), block-scan wave sums after
   unsigned long long* sortk;  // [max(N, n_perm_slots)] sort keys
   int* perm;        // [n_perm_slots]
   unsigned long long* dmin;  // [R+3]
@@ -110,7 +110,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(csr, N * 4)
   TAKE(cand, RN * 4)
   TAKE(ckey, RN * 4)
-  TAKE(iscal, 16 * 4)
+  TAKE(iscal, (16 + SURV_TMAX / 64) * 4)
   TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
   TAKE(perm, (size_t)Pperm * 4)
   TAKE(dmin, (size_t)RN * 8)
@@ -464,7 +464,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   PHASE(2)
 
   // ---- fast non-dominated sort (discovery order), stop once >= n_survive ranked
-  int* wsum = L.iscal;  // [0..3]
+  int* wsum = L.iscal + 16;  // one int per wave (iscal[15] is the association counter)
   int n0 = block_compact<T>(
       N,
       [&](int j) {
