@@ -360,22 +360,29 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   __syncthreads();
   PHASE(1)
 
-  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population
-  {
+  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: one
+  // wave, while the other waves start the dominance pass below (independent of it; its
+  // results are first read after the pass's barrier).  min/max of these values do not
+  // depend on the reduction order (NaN propagates either way; no -0.0 objective exists:
+  // f1 is a probability, f2 a sqrt, f3 a sum starting at +0.0).  Above SURV_NLDS (HBM
+  // bitsets, N^2 work 10x the headline's) the dominance pass keeps every wave: ideal/worst
+  // first, then a barrier.
+  const bool iw_overlap = N <= SURV_NLDS;
+  if (wave == 0) {
     double mn[3], mx[3], wp[3];
     for (int k = 0; k < 3; ++k) {
       mn[k] = __builtin_inf();
       mx[k] = -__builtin_inf();
       wp[k] = -__builtin_inf();
     }
-    for (int m = tid; m < N; m += T)
+    for (int m = lane; m < N; m += 64)
       for (int k = 0; k < 3; ++k) {
         const double v = L.F[m * 3 + k];
         mn[k] = min_prop(mn[k], v);
         mx[k] = max_prop(mx[k], v);
         wp[k] = max_prop(wp[k], v);
       }
-    for (int r = tid; r < R; r += T)
+    for (int r = lane; r < R; r += 64)
       for (int k = 0; k < 3; ++k) {
         const double v = L.ref[r * 3 + k];
         mn[k] = min_prop(mn[k], v);
@@ -386,27 +393,24 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       mx[k] = wred_max(mx[k]);
       wp[k] = wred_max(wp[k]);
     }
-    if (lane == 0)
-      for (int k = 0; k < 3; ++k) {
-        L.red[wave * 16 + k] = mn[k];
-        L.red[wave * 16 + 3 + k] = mx[k];
-        L.red[wave * 16 + 6 + k] = wp[k];
+    if (lane < 3) {
+      const int k = lane;
+      double vmn = mn[0], vmx = mx[0], vwp = wp[0];
+      if (k == 1) {
+        vmn = mn[1];
+        vmx = mx[1];
+        vwp = wp[1];
+      } else if (k == 2) {
+        vmn = mn[2];
+        vmx = mx[2];
+        vwp = wp[2];
       }
-    __syncthreads();
-    if (tid < 3) {
-      const int k = tid;
-      double vmn = pre_ideal, vmx = pre_worst;
-      double vwp = -__builtin_inf();
-      for (int w = 0; w < T / 64; ++w) {
-        vmn = min_prop(vmn, L.red[w * 16 + k]);
-        vmx = max_prop(vmx, L.red[w * 16 + 3 + k]);
-        vwp = max_prop(vwp, L.red[w * 16 + 6 + k]);
-      }
-      ideal[k] = vmn;
-      worst[k] = vmx;
+      ideal[k] = min_prop(pre_ideal, vmn);
+      worst[k] = max_prop(pre_worst, vmx);
       wpop[k] = vwp;
     }
   }
+  if (!iw_overlap) __syncthreads();
   PHASE(11)
 
   // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the
@@ -418,7 +422,8 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   {
     unsigned* dom32 = (unsigned*)L.dom;
     const int n_items = NW * (NW + 1);
-    for (int t = wave; t < n_items; t += T / 64) {
+    const int w0 = iw_overlap ? 1 : 0;  // first dominance wave (wave 0: ideal/worst)
+    for (int t = wave - w0; wave >= w0 && t < n_items; t += T / 64 - w0) {
       const int h = t & 1;
       int qi = 0, rem = t >> 1;
       while (rem >= NW - qi) {
