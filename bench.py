@@ -351,7 +351,8 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of THIS workload and
     # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
-    tpath = os.path.join(ROOT, "profiles", "r02", f"pmc_traffic_{args.workload}_{args.mode}.json")
+    tpath = os.path.join(ROOT, "profiles", "r02",
+                         f"pmc_traffic_{args.workload}_{'whole' if whole else 'chain'}.json")
     if os.path.exists(tpath) and args.crossover == "two_point" and not bf16:
         with open(tpath) as fh:
             traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()
