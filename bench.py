@@ -203,6 +203,19 @@ def data_note(w, B):
     return f"{src[w['project']]} ({how}) + {clf} and shipped scaler"
 
 
+def load_traffic(workload, whole):
+    """Per-kernel HBM bytes per launch from the committed rocprofv3 PMC passes of `workload`
+    under the schedule that actually ran (`whole`: one-launch attack, else the kernel chain);
+    {} when that workload/schedule was never measured."""
+    path = os.path.join(ROOT, "profiles", "r02",
+                        f"pmc_traffic_{workload}_{'whole' if whole else 'chain'}.json")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as fh:
+        return {k: v["traffic_bytes"] for k, v in json.load(fh).items()
+                if isinstance(v, dict) and "traffic_bytes" in v}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -351,12 +364,8 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of THIS workload and
     # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
-    tpath = os.path.join(ROOT, "profiles", "r02",
-                         f"pmc_traffic_{args.workload}_{'whole' if whole else 'chain'}.json")
-    if os.path.exists(tpath) and args.crossover == "two_point" and not bf16:
-        with open(tpath) as fh:
-            traffic = {k: v["traffic_bytes"] for k, v in json.load(fh).items()
-                       if isinstance(v, dict) and "traffic_bytes" in v}
+    if args.crossover == "two_point" and not bf16:
+        traffic = load_traffic(args.workload, whole)
 
     def hbm(name, bytes_launch, ms, key):
         gbs = bytes_launch / (ms * 1e-3) / 1e9

@@ -1,0 +1,19 @@
+"""bench.py host logic that needs no GPU: the roofline `traffic` lookup."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_headline_traffic_is_attached_to_the_chain_schedule():
+    t = bench.load_traffic("rq1.botnet.static", whole=False)
+    assert set(t) >= {"k_gen", "k_cons", "k_mlp", "k_survive"}
+    assert all(v > 0 for v in t.values())
+
+
+def test_unmeasured_workload_or_schedule_gets_no_traffic():
+    assert bench.load_traffic("rq1.botnet.static", whole=True) == {}
+    assert bench.load_traffic("synthetic.botnet.wide", whole=False) == {}
