@@ -9,12 +9,13 @@ step   : one full MoEvA2 attack (all states, n_gen generations: init + evaluate,
 workload (N=1): configs[1] = rq1.botnet.static -- the 387 shipped CTU-13 botnet states,
          n_pop 200 (P = 203), n_offsprings 100, budget 1000 generations, L2, history
          "reduced" (config/moeva.yaml, config/rq1.botnet.static.yaml, config/rq1.botnet.yaml).
-multi-GPU: states are independent (moeva2.py:194-205).  Default (weak scaling): every rank
-         attacks the workload's full state set with its own seed (seed 42 + rank: N
-         independent attack replicas), no collective inside the attack; one all_gather of
-         the per-state best misclassification value closes the step.  --shard (strong
-         scaling): the states are split over the ranks (moeva2_amd.distributed.shard_bounds,
-         as Moeva2.generate_sharded), each rank attacks its slice, one all_gather.
+multi-GPU: states are independent (moeva2.py:194-205).  Every step runs
+         Moeva2.generate_sharded's path (moeva2_amd.distributed): rank r attacks its
+         contiguous shard of the state set, no collective inside the attack, one
+         all_gather of the final populations (genes + objectives) closes the step.
+         Default (weak scaling): the workload's state set tiled x N, so every rank attacks
+         one full copy.  --shard (strong scaling): the workload's states split over the
+         ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--shard]
                     [--mode auto|chain|whole] [--crossover two_point|sbx]
@@ -89,6 +90,13 @@ def load_states(w):
     if n is not None:
         X = X[:n] if n <= X.shape[0] else np.resize(X, (n, X.shape[1]))
     return np.ascontiguousarray(X)
+
+def global_states(X_all, world, shard):
+    """The state set one step attacks over all ranks: the workload's states (strong
+    scaling, --shard) or the workload's states tiled x world (weak scaling: rank r's
+    shard_bounds slice is copy r)."""
+    return X_all if shard else np.concatenate([X_all] * world)
+
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 MFMA_F32_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA (= f32 vector peak)
@@ -257,7 +265,7 @@ def main():
         w["n_gen"] = args.n_gen
     from moeva2_amd.attacks.moeva2.moeva2 import history_mode
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
-    from moeva2_amd.distributed import all_gather_states, shard_bounds
+    from moeva2_amd.distributed import generate_sharded, shard_bounds
 
     t_load = time.perf_counter()
     eng, c = build_engine(w, device)
@@ -266,37 +274,42 @@ def main():
     eng.set_mlp_precision(args.mlp_dtype)
     bf16 = args.mlp_dtype == "bf16"
     X_all = load_states(w)
+    # weak scaling (default): the workload's state set tiled x N (rank r owns copy r);
+    # strong (--shard): the workload's states split over the ranks.  Either way the step is
+    # Moeva2.generate_sharded's path: each rank attacks its contiguous shard
+    # (distributed.shard_bounds) and one all_gather returns every state's final population
+    # (genes + objectives) to every rank (RCCL over xGMI).
+    X_glob = global_states(X_all, world, args.shard)
     B_all = X_all.shape[0]
-    lo, hi = shard_bounds(B_all, world, rank) if args.shard else (0, B_all)
-    X = X_all[lo:hi]
+    states_total = X_glob.shape[0]
+    lo, hi = shard_bounds(states_total, world, rank)
+    X = X_glob[lo:hi]
     B = X.shape[0]
-    if B == 0:
-        raise SystemExit(f"rank {rank}: no states in its shard ({B_all} states, {world} ranks)")
-    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
-    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    if B:
+        bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+        eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]),
+                       1)
     ref = energy_ref_dirs(3, w["n_pop"], seed=1)
     P, O, G = w["n_pop"] + 3, w["n_off"], w["n_gen"]
     hmode = history_mode(w["history"])
     V = eng.prog.V
     genes = torch.empty((B, P, V), dtype=torch.float64, device="cuda")
     F = torch.empty((B, P, 3), dtype=torch.float64, device="cuda")
-    gathered = torch.empty((world, B), dtype=torch.float64, device="cuda")
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
-    # weak: every rank attacks the whole state set, rank r with seed 42 + r (replicas);
-    # strong (--shard): one seed, the states split over the ranks (generate_sharded)
-    seed = 42 if args.shard else 42 + rank
+    seed = 42  # the configs' seed, every state (moeva2.py:163)
 
-    def step():
+    def attack(xs, mcs):  # the rank's shard is bound once, outside the timed region
+        assert xs.shape[0] == B
         eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
         eng.attack_population(genes, F)
-        best = F[:, :, 0].min(dim=1).values.contiguous()
-        if world > 1 and args.shard:
-            all_gather_states(best, B_all)
-        elif world > 1:
-            dist.all_gather_into_tensor(gathered, best)
-        else:
-            gathered[0].copy_(best)
+        return genes, F
+
+    def empty():
+        return genes[:0], F[:0]
+
+    def step():
+        return generate_sharded(attack, X_glob, 1, empty=empty)
 
     for i in range(args.warmup):
         step()
@@ -307,7 +320,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
+        out = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -316,10 +329,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    assert out[0].shape == (states_total, P, V)
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed:.3f}s")
 
     evals_per_state = P + (G - 1) * O
-    states_total = B_all if args.shard else world * B_all
     total_evals = states_total * evals_per_state * args.steps
     value = total_evals / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -327,6 +340,10 @@ def main():
     # ---- roofline of the dominant kernel, measured live with HIP events that the engine
     # records on the bench stream around every launch (one state group, so each launch
     # covers all states of the rank like the rocprofv3 pass of the same command)
+    if rank != 0:  # only rank 0 reports (it always owns states); the others are done
+        if world > 1:
+            dist.destroy_process_group()
+        return
     eng.set_profiling(True)
     eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
@@ -377,7 +394,9 @@ def main():
         n_launch_evals = B * evals_per_state
         kernels = {"k_attack": hbm("k_attack (whole attack: one launch, one workgroup per "
                                    "state)", eval_bytes * n_launch_evals, att_ms, "k_attack")}
-        kernels["k_attack"]["mfma_tflops"] = eval_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
+        kernels["k_attack"]["mfma_tflops"] = exec_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
+        kernels["k_attack"]["mfma_tflops_algorithmic"] = \
+            eval_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
         per_gen = {"k_attack_ms_per_attack": att_ms, "dominant": "k_attack"}
     else:
         ng = max(kt["generations"], 1)
@@ -385,7 +404,10 @@ def main():
         cons_ms = kt["cons_ms"] / ng
         mlp_ms = kt["mlp_ms"] / ng
         surv_ms = kt["survive_ms"] / ng
-        mlp_tfs = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
+        # achieved / frac on the FLOPs the kernel executes (immutable features folded into
+        # the per-state bias); the full-chain algorithmic rate is reported beside it
+        mlp_tfs = exec_flops * rows / (mlp_ms * 1e-3) / 1e12
+        mlp_tfs_alg = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
         mlp_peak = MFMA_BF16_PEAK_TFS if bf16 else MFMA_F32_PEAK_TFS
         kernels = {
             "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows,
@@ -396,6 +418,7 @@ def main():
                       "unit": "TFLOP/s", "frac": mlp_tfs / mlp_peak,
                       "traffic": traffic.get("k_mlp"),
                       "kernel": "k_mlp (%s MFMA Dense chain)" % ("bf16" if bf16 else "fp32"),
+                      "achieved_algorithmic": mlp_tfs_alg,
                       "algorithmic_flops_per_launch": eval_flops * rows,
                       "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},
             "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
@@ -420,11 +443,11 @@ def main():
         per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
     dom = per_gen["dominant"]
     if args.shard:
-        par = (f"states sharded over {world} rank(s): {B} of {B_all} on rank {rank}; one "
-               "all_gather of per-state results")
+        par = (f"generate_sharded: {B_all} states split over {world} rank(s) ({B} on rank "
+               f"{rank}); one all_gather of the final populations")
     else:
-        par = (f"{world} rank(s), each attacking all {B_all} states with its own seed "
-               "(independent replicas); one all_gather of per-state results")
+        par = (f"generate_sharded: the {B_all} states tiled x{world} = {states_total}, "
+               f"{B} per rank; one all_gather of the final populations")
 
     result = {
         "metric": "candidate fitness evals/sec (whole node) + attack wall-clock per 1k states",
@@ -439,7 +462,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": data_note(w, B_all),
-        "config": {"workload": args.workload, "states": B_all, "states_per_gpu": B,
+        "config": {"workload": args.workload, "states": states_total, "states_per_gpu": B,
                    "pop_size": P, "n_offsprings": O, "n_gen": G, "norm": w["norm"],
                    "history": w["history"], "evals_per_state": evals_per_state,
                    "classifier_dtype": ("bf16 perf mode (bf16 MFMA, fp32 accumulate; not a "

@@ -179,6 +179,15 @@ void mv_objcalc_destroy(mv_objcalc* o);
 int mv_objcalc_run(mv_objcalc* o, mv_engine* constraints, mv_mlp* classifier, int32_t B,
                    int32_t n, const double* x_init, const double* x, int32_t minimize_class,
                    double* obj, int32_t* range_bad, void* stream);
+/* The same scoring with the constraint matrix and / or the class probabilities supplied by
+ * the caller (device buffers): G dev [B*n][C] (Constraints.evaluate(x_f), C >= 0) and proba
+ * dev [B*n][n_out].  This is the plugin path of ObjectiveCalculator._calculate_objective
+ * (objective_calculator.py:44-84) for a Constraints subclass without a device program or a
+ * predict_proba model that is not a Dense MLP: the host evaluates the plugin, the device
+ * does the one-hot term, the CV sum, the ML/min-max scaling checks and the distance. */
+int mv_objcalc_score(mv_objcalc* o, int32_t B, int32_t n, const double* x_init, const double* x,
+                     const double* G, int32_t C, const double* proba, int32_t n_out,
+                     int32_t minimize_class, double* obj, int32_t* range_bad, void* stream);
 typedef struct mv_attack_params {
   int32_t n_gen;          /* Moeva2 n_gen (termination "n_gen") */
   int32_t pop_size;       /* P = n_ref_points + n_obj (203 for n_pop 200) */

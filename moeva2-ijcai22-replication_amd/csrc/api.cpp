@@ -1284,6 +1284,41 @@ int mv_objcalc_run(mv_objcalc* o, mv_engine* e, mv_mlp* m, int32_t B, int32_t n,
   return MV_OK;
 }
 
+int mv_objcalc_score(mv_objcalc* o, int32_t B, int32_t n, const double* x_init, const double* x,
+                     const double* G, int32_t C, const double* proba, int32_t n_out,
+                     int32_t minimize_class, double* obj, int32_t* range_bad, void* stream_) {
+  if (!o || B < 0 || n < 0 || C < 0 || n_out < 1)
+    return fail(MV_ERR_ARG, "bad mv_objcalc_score arguments");
+  if (minimize_class < 0 || minimize_class >= (n_out == 1 ? 2 : n_out))
+    return fail(MV_ERR_ARG, "minimize_class outside the classifier output");
+  const long total = (long)B * n;
+  if (total == 0) return MV_OK;
+  if (!x_init || !x || !obj || !range_bad || !proba || (C > 0 && !G))
+    return fail(MV_ERR_ARG, "null buffer");
+  HIPCHK(hipSetDevice(o->device));
+  ObjArgs a{};
+  a.total = total;
+  a.n = n;
+  a.D = o->D;
+  a.C = C;
+  a.n_ohe = o->n_ohe;
+  a.n_out = n_out;
+  a.cls = minimize_class;
+  a.norm = o->norm;
+  a.x = x;
+  a.x_init = x_init;
+  a.mm_scale = o->mm_s;
+  a.mm_min = o->mm_m;
+  a.ohe_off = o->ohe_off;
+  a.ohe_feat = o->ohe_feat;
+  a.G = G;
+  a.proba = proba;
+  a.obj = obj;
+  a.range_bad = range_bad;
+  HIPCHK(launch_objectives(a, (hipStream_t)stream_));
+  return MV_OK;
+}
+
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
   if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
   HIPCHK(hipSetDevice(e->device));

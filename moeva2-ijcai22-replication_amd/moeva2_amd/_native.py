@@ -28,7 +28,7 @@ EXPORTED = [
     "mv_set_crossover", "mv_set_mlp_precision",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
-    "mv_det_pow",
+    "mv_objcalc_score", "mv_det_pow",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -108,6 +108,8 @@ def lib():
             "mv_mlp_predict": [vp, C.c_int32, vp, vp, vp],
             "mv_objcalc_create": [C.c_int32, C.POINTER(ObjCalcDesc), C.POINTER(vp)],
             "mv_objcalc_run": [vp, vp, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp, vp, vp],
+            "mv_objcalc_score": [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_int32, vp, C.c_int32,
+                                 C.c_int32, vp, vp, vp],
             "mv_det_pow": [C.c_int64, _f64p, _f64p, _f64p],
         }
         for name, args in sig.items():
@@ -267,7 +269,7 @@ class Engine:
     def set_states(self, x_init, xl, xu, minimize_class, stream=None, owner=None):
         """Bind B initial states (mv_set_states).  ``owner`` tags the binding so a caller
         that evaluates repeatedly on the same states (DefaultProblem) binds only once."""
-        self.bound_by = owner
+        self.bound_by = None
         x_init = _arr(x_init, np.float64)
         xl = _arr(xl, np.float64)
         xu = _arr(xu, np.float64)
@@ -277,6 +279,7 @@ class Engine:
                                   xu.ctypes.data_as(_f64p), mc.ctypes.data_as(_i32p),
                                   _stream(stream)))
         self.B = x_init.shape[0]
+        self.bound_by = owner  # only once the engine holds these states
 
     def evaluate(self, genes, F, G=None, stream=None):
         """genes (B, n, V) fp64 device tensor -> F (B, n, 3) [, G (B, n, C)]."""
@@ -453,6 +456,15 @@ class ObjCalc:
         check(lib().mv_objcalc_run(self._h, engine._h, mlp._h, B, n, _ptr(x_init), _ptr(x),
                                    int(minimize_class), _ptr(obj), _ptr(range_bad),
                                    _stream(stream)))
+
+    def score(self, x_init, x, G, proba, minimize_class, obj, range_bad, stream=None):
+        """Scoring with a caller-supplied constraint matrix G (B*n, C) (None: C = 0) and
+        class probabilities proba (B*n, n_out), all device tensors (mv_objcalc_score)."""
+        B, n = int(x.shape[0]), int(x.shape[1])
+        C_ = 0 if G is None else int(G.shape[-1])
+        check(lib().mv_objcalc_score(self._h, B, n, _ptr(x_init), _ptr(x), _ptr(G), C_,
+                                     _ptr(proba), int(proba.shape[-1]), int(minimize_class),
+                                     _ptr(obj), _ptr(range_bad), _stream(stream)))
 
 
 _MLPS = {}

@@ -39,13 +39,15 @@ class ObjectiveCalculator:
 
     # -- device objects (built on first use)
     def _device(self):
+        """(ObjCalc, constraint engine or None, device classifier or None).  A Constraints
+        object without a device program, or a classifier that is not a Dense MLP, is
+        evaluated through its own ``evaluate`` / ``predict_proba`` on the host (the
+        reference accepts any plugin, objective_calculator.py:44-64); the one-hot term, CV
+        sum, scaling checks and distance stay on the device (mv_objcalc_score)."""
         if self._dev is None:
             from ..._native import Mlp, ObjCalc
+            from ...problem import has_device_classifier, has_device_program
 
-            if not hasattr(self._classifier, "dense_weights"):
-                raise NotImplementedError("the device ObjectiveCalculator needs a Dense-MLP "
-                                          "Classifier (attacks.moeva2.classifier.load_model)")
-            mlp = self._classifier.dense_weights()
             masks = get_ohe_masks(self._constraints.get_feature_type())
             D = int(self._constraints.get_feature_type().shape[0])
             mls = self._ml_scaler
@@ -55,8 +57,15 @@ class ObjectiveCalculator:
                          None if mls is None else np.asarray(mls.scale_, np.float64),
                          None if mls is None else np.asarray(mls.min_, np.float64),
                          self.norm)
-            self._dev = (oc, self._constraints._constraint_engine(),
-                         Mlp(mlp.weights, mlp.biases))
+            ceng = None
+            if (hasattr(self._constraints, "_constraint_engine")
+                    and has_device_program(self._constraints)):
+                ceng = self._constraints._constraint_engine()
+            mlp = None
+            if has_device_classifier(self._classifier):
+                w = self._classifier.dense_weights()
+                mlp = Mlp(w.weights, w.biases)
+            self._dev = (oc, ceng, mlp)
         return self._dev
 
     def calculate_objectives_3d(self, x_initials, x):
@@ -66,20 +75,42 @@ class ObjectiveCalculator:
         calls it with B = 1)."""
         import torch
 
+        from ...problem import ml_transform
+
         x_initials = np.ascontiguousarray(np.atleast_2d(x_initials), np.float64)
         x = np.ascontiguousarray(x, np.float64)
         if x.ndim != 3 or x.shape[0] != x_initials.shape[0] or x.shape[2] != x_initials.shape[1]:
             raise ValueError(f"x {x.shape} and x_initials {x_initials.shape} do not match")
-        B, n, _ = x.shape
+        B, n, D = x.shape
         if B * n == 0:
             return np.zeros((B, n, 3))
-        oc, eng, mlp = self._device()
+        oc, ceng, mlp = self._device()
         dev = torch.device("cuda", oc.device)
         xi = torch.from_numpy(x_initials).to(dev)
         xd = torch.from_numpy(x).to(dev)
         obj = torch.empty((B, n, 3), dtype=torch.float64, device=dev)
         bad = torch.empty((B, n), dtype=torch.int32, device=dev)
-        oc.run(eng, mlp, xi, xd, self._minimize_class, obj, bad)
+        if ceng is not None and mlp is not None:
+            oc.run(ceng, mlp, xi, xd, self._minimize_class, obj, bad)
+        else:
+            x_f = x.reshape(B * n, D)
+            if ceng is not None:
+                G = torch.empty((B * n, ceng.prog.C), dtype=torch.float64, device=dev)
+                if ceng.prog.C > 0:
+                    ceng.constraints(xd.view(B * n, D), G)
+            else:  # objective_calculator.py:50: the plugin's own numpy evaluate
+                g = np.ascontiguousarray(self._constraints.evaluate(x_f), np.float64)
+                G = torch.from_numpy(g.reshape(B * n, -1)).to(dev)
+            x_ml = ml_transform(self._ml_scaler, x_f)  # :61-63
+            if mlp is not None:
+                xm = torch.from_numpy(np.ascontiguousarray(x_ml, np.float64)).to(dev)
+                proba = torch.empty((B * n, mlp.n_out), dtype=torch.float64, device=dev)
+                mlp.predict(xm, proba)
+            else:  # :64 Classifier.predict_proba of any model
+                p = np.ascontiguousarray(self._classifier.predict_proba(x_ml), np.float64)
+                proba = torch.from_numpy(p.reshape(B * n, -1)).to(dev)
+            oc.score(xi, xd, G if G.shape[1] > 0 else None, proba, self._minimize_class, obj,
+                     bad)
         # objective_calculator.py:72-76: the scaled origin and candidates must lie in [0, 1]
         assert not bool(bad.any().item()), "candidate or initial state outside the scaler range"
         return obj.cpu().numpy()

@@ -54,10 +54,12 @@ def generate_sharded(attack: Callable, x: np.ndarray, minimize_class, group=None
     shapes `attack` returns -- so every rank still enters the same all_gather."""
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
     B = x.shape[0]
     mc = np.broadcast_to(np.asarray(minimize_class), (B,))
+    if not (dist.is_available() and dist.is_initialized()):  # one process: no collective
+        return tuple(attack(x, mc))
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     lo, hi = shard_bounds(B, world, rank)
     if hi > lo or empty is None:
         outs = attack(x[lo:hi], mc[lo:hi])

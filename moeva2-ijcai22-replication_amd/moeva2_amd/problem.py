@@ -12,6 +12,8 @@ def has_device_program(constraints) -> bool:
     """True when the Constraints object describes its numpy path as a device program (the
     shipped LCLD / botnet classes); any other subclass is evaluated by its own ``evaluate``
     on the host (SURVEY.md §8b plugin fallback)."""
+    if not callable(getattr(constraints, "device_program", None)):
+        return False  # a duck-typed plugin that does not derive from our Constraints
     try:
         constraints.device_program()
         return True

@@ -418,52 +418,48 @@ def evaluate(prob: Problem, genes: np.ndarray, return_g=False):
 # E. R-NSGA-III survival  [pymoo-recall except the dominance relation]
 # --------------------------------------------------------------------------------------
 def domination_matrix(F: np.ndarray) -> np.ndarray:
-    """pareto_operation.py ``calc_domination_matrix`` (copy of pymoo Dominator), epsilon 0."""
-    n = F.shape[0]
-    L = np.repeat(F, n, axis=0)
-    R = np.tile(F, (n, 1))
-    smaller = np.reshape(np.any(L < R, axis=1), (n, n))
-    larger = np.reshape(np.any(L > R, axis=1), (n, n))
+    """pareto_operation.py ``calc_domination_matrix`` (copy of pymoo Dominator), epsilon 0.
+    The reference builds L = repeat(F), R = tile(F) and compares row pairs; the broadcast
+    below compares the same pairs (i, j) -> (F[i], F[j])."""
+    smaller = np.zeros((F.shape[0], F.shape[0]), dtype=bool)
+    larger = np.zeros_like(smaller)
+    for k in range(F.shape[1]):
+        a, b = F[:, k, None], F[None, :, k]
+        smaller |= a < b
+        larger |= a > b
     return (np.logical_and(smaller, ~larger) * 1 + np.logical_and(larger, ~smaller) * -1)
 
 
 def fast_non_dominated_sort(F: np.ndarray, n_stop_if_ranked: int):
     """[pymoo-recall] NonDominatedSorting().do(F, return_rank=True, n_stop_if_ranked)
-    with the fast-non-dominated-sort discovery order."""
+    with the fast-non-dominated-sort discovery order.
+
+    pymoo's loop (for i, for j > i: append the dominated index to ``is_dom[dominator]``)
+    leaves ``is_dom[i]`` = the indices i dominates in increasing order, and front 0 = the
+    undominated indices in increasing order.  Each later front lists j in the order its
+    counter reaches zero while the previous front is walked in order: by the position of
+    j's last dominator in that front, then by j.  That order is computed here array-wise
+    (tests/test_oracle_survival_cpu.py pins it to the literal loop)."""
     M = domination_matrix(F)
     n = M.shape[0]
-    is_dom = [[] for _ in range(n)]
-    n_dom = np.zeros(n, dtype=np.int64)
-    fronts = []
-    cur = []
-    ranked = 0
-    for i in range(n):
-        for j in range(i + 1, n):
-            r = M[i, j]
-            if r == 1:
-                is_dom[i].append(j)
-                n_dom[j] += 1
-            elif r == -1:
-                is_dom[j].append(i)
-                n_dom[i] += 1
-        if n_dom[i] == 0:
-            cur.append(i)
-            ranked += 1
-    fronts.append(cur)
+    D = M == 1  # D[i, j]: i dominates j
+    n_dom = D.sum(axis=0)
+    cur = np.flatnonzero(n_dom == 0)
+    fronts = [cur]
+    ranked = len(cur)
     while ranked < n:
-        nxt = []
-        for i in cur:
-            for j in is_dom[i]:
-                n_dom[j] -= 1
-                if n_dom[j] == 0:
-                    nxt.append(j)
-                    ranked += 1
-        fronts.append(nxt)
-        cur = nxt
+        Dc = D[cur]
+        dec = Dc.sum(axis=0)
+        n_dom = n_dom - dec
+        newly = np.flatnonzero((n_dom == 0) & (dec > 0))
+        last = (len(cur) - 1) - np.argmax(Dc[::-1][:, newly], axis=0)
+        cur = newly[np.lexsort((newly, last))]
+        fronts.append(cur)
+        ranked += len(cur)
     out = []
     nr = 0
     for f in fronts:
-        out.append(np.array(f, dtype=np.int64))
+        out.append(np.asarray(f, dtype=np.int64))
         nr += len(f)
         if nr >= n_stop_if_ranked:
             break
@@ -549,10 +545,37 @@ def nadir_point(extreme, ideal, worst, worst_of_front_arg, worst_of_population_a
 
 
 def ref_dirs_from_points(ref_point, asp_dirs, mu):
-    """[pymoo-recall] rnsga3.get_ref_dirs_from_points + line_plane_intersection."""
+    """[pymoo-recall] rnsga3.get_ref_dirs_from_points + line_plane_intersection.
+    With one aspiration direction (MoEvA2's, ``moeva2.py``'s 1x3 (1/3, 1/3, 1/3)) the
+    per-point loop is evaluated for all points at once with the same operations."""
     n_obj = ref_point.shape[1]
     nvec = np.ones(n_obj) / np.sqrt(n_obj)
     p0 = np.eye(n_obj)[0]
+    asp = np.asarray(asp_dirs, dtype=np.float64)
+    if asp.shape[0] == 1 and n_obj == 3:
+        P = np.asarray(ref_point, dtype=np.float64)
+        r0 = mu * asp[0]
+        cent = r0 / 1.0  # np.mean over one row
+        l = P - 0.0
+        dot = (l[:, 0] * nvec[0] + l[:, 1] * nvec[1]) + l[:, 2] * nvec[2]
+        w = p0 - 0.0
+        wn = (w[0] * nvec[0] + w[1] * nvec[1]) + w[2] * nvec[2]
+        big = np.abs(dot) > 1e-6
+        with np.errstate(divide="ignore", invalid="ignore"):
+            d = wn / dot
+            inter_a = 0.0 + l * d[:, None]
+        q = P - p0
+        t = (q[:, 0] * nvec[0] + q[:, 1] * nvec[1]) + q[:, 2] * nvec[2]
+        inter_b = P - t[:, None] * nvec
+        inter = np.where(big[:, None], inter_a, inter_b)
+        r = r0[None, :] + (inter - cent[None, :])
+        fix = ~(r > 0).min(axis=1)
+        if fix.any():
+            rf = r[fix]
+            rf[rf < 0] = 0
+            s = (rf[:, 0] + rf[:, 1]) + rf[:, 2]
+            r[fix] = rf / s[:, None]
+        return np.concatenate([r, np.eye(n_obj)])
     val = []
     for point in ref_point:
         r = mu * np.array(asp_dirs, dtype=np.float64, copy=True)
@@ -609,6 +632,7 @@ def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
       shuffle per round) and picks in the order of one random permutation have the same
       distribution; fixing the keys makes each niche's pick order a single sort."""
     niche_count = np.array(niche_count, dtype=np.int64, copy=True)
+    niche_of = np.asarray(niche_of)
     L = len(niche_of)
     n_niches = len(niche_count)
     mask = np.ones(L, dtype=bool)
@@ -617,16 +641,25 @@ def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
     sp = px.Stream(seed, gen, px.TAG_NICHE_PERM, stream_key)
     sm = px.Stream(seed, gen, px.TAG_NICHE_MEMBER, stream_key)
     km = sm.words(np.arange(L))[0].astype(np.int64)
+    # members of each niche in increasing position (np.where order)
+    by_niche = np.argsort(niche_of, kind="stable")
+    starts = np.searchsorted(niche_of[by_niche], np.arange(n_niches + 1))
+    # niche-order keys are drawn for blocks of rounds at once (same counters)
+    kblk, k0, KB = None, -1, 8
     while len(survivors) < n_remaining:
         n_select = n_remaining - len(survivors)
         nl = np.unique(niche_of[mask])
         cnt = niche_count[nl]
         cand = nl[cnt == cnt.min()]
-        kn = sp.words(rnd * n_niches + cand)[0].astype(np.int64)
+        if kblk is None or rnd >= k0 + KB:
+            k0 = rnd
+            kblk = sp.words(np.arange(k0 * n_niches, (k0 + KB) * n_niches))[0].astype(np.int64)
+        kn = kblk[(rnd - k0) * n_niches + cand]
         order = np.lexsort((cand, kn))
         cand = cand[order][:n_select]
         for nn in cand:
-            members = np.where((niche_of == nn) & mask)[0]
+            members = by_niche[starts[nn]:starts[nn + 1]]
+            members = members[mask[members]]
             if niche_count[nn] == 0:
                 dmin = dist[members].min()
                 members = members[dist[members] == dmin]

@@ -8,6 +8,8 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _free_port():
     s = socket.socket()
@@ -73,3 +75,63 @@ def test_sharded_attack_gathers_every_state(B, world):
     per = -(-B // world)
     assert [shard_bounds(B, world, r) for r in range(world)] == \
         [(min(r * per, B), min(r * per + per, B)) for r in range(world)]
+
+
+def _bench_worker(rank, world, port, B_all, shard, q):
+    """bench.py's step on a gloo group: the rank's shard of global_states is bound once
+    (the engine rejects B = 0: mv_set_states), the attack must be called with exactly that
+    shard, and generate_sharded gathers every state's result on every rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    from bench import global_states
+    from moeva2_amd.distributed import generate_sharded, shard_bounds
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X_all = np.arange(B_all * 5, dtype=np.float64).reshape(B_all, 5)
+    X_glob = global_states(X_all, world, shard)
+    lo, hi = shard_bounds(X_glob.shape[0], world, rank)
+    bound = X_glob[lo:hi]
+    calls = []
+
+    def attack(xs, mc):
+        assert len(bound) > 0 and np.array_equal(xs, bound)  # the engine's input contract
+        calls.append(len(xs))
+        return fake_attack(xs, mc)
+
+    outs = [generate_sharded(attack, X_glob, 1, empty=fake_empty) for _ in range(2)]
+    q.put((rank, calls, [o[0].numpy() for o in outs], X_glob))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B_all,world,shard", [(5, 2, False), (5, 2, True), (1, 2, True),
+                                               (3, 3, False)])
+def test_bench_step_is_generate_sharded(B_all, world, shard):
+    """bench.py --gpus N times generate_sharded: weak scaling tiles the states x N (one copy
+    per rank), strong scaling (--shard) splits them, an empty rank joins the all_gather."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, B_all, shard, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    n_glob = B_all if shard else B_all * world
+    for rank, calls, outs, X_glob in res:
+        assert X_glob.shape[0] == n_glob
+        ref_g, _ = fake_attack(X_glob, np.ones(n_glob))
+        for g in outs:
+            np.testing.assert_array_equal(g, ref_g.numpy())
+        per = -(-n_glob // world)
+        mine = max(0, min(n_glob, (rank + 1) * per) - rank * per)
+        assert calls == ([mine] * 2 if mine else [])

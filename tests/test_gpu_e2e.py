@@ -87,6 +87,110 @@ def _e2e(fixture):
     return sr_dev, sr_ref, best, d["best_f1"]
 
 
+DEVICE_SEEDS = list(range(1000, 1032))  # disjoint from make_e2e_seeds.py's SEED0 = 100 + k
+
+
+def _device_seed_rates(name, B, n_gen, n_pop, n_off, eps, thr, seeds):
+    """Device attack at every seed, scored like 04_moeva.py:112-131: final populations
+    decoded on the device (FeatureEncoder.genetic_to_ml) and scored by the package's
+    ObjectiveCalculator (objective_calculator.py:44-119, pinned by
+    tests/golden/objective_calculator_botnet.npz).  Returns respected (S, B, 7) and the
+    genes / ML rows of the first seed (cross-checked against the oracle's scoring)."""
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, load_model
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+    from moeva2_amd.experiments.united.utils import STR_TO_CONSTRAINTS_CLASS
+    from moeva2_amd.problem import get_engine
+
+    p = Project(name)
+    X = p.x[:B]
+    feat = os.path.join(RES, PROJECTS[name][0])
+    c = STR_TO_CONSTRAINTS_CLASS[name](feat, feat.replace("features", "constraints"))
+    model = load_model(os.path.join(RES, PROJECTS[name][1]))
+    scaler = NpScaler(os.path.join(RES, PROJECTS[name][2]))
+    eng = get_engine(c, Classifier(model), scaler, 2)
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    calc = ObjectiveCalculator(Classifier(model), c, 1, {"f1": thr, "f2": eps},
+                               min_max_scaler=scaler, ml_scaler=scaler, norm=2)
+    oc, ceng, mlp = calc._device()
+    P = n_pop + 3
+    ref = energy_ref_dirs(3, n_pop, seed=1)
+    dev = torch.device("cuda")
+    g = torch.empty((B, P, eng.prog.V), dtype=torch.float64, device=dev)
+    x = torch.empty((B, P, X.shape[1]), dtype=torch.float64, device=dev)
+    xi = torch.from_numpy(np.ascontiguousarray(X)).to(dev)
+    obj = torch.empty((B, P, 3), dtype=torch.float64, device=dev)
+    bad = torch.empty((B, P), dtype=torch.int32, device=dev)
+    resp = np.zeros((len(seeds), B, 7), bool)
+    first = None
+    for k, s in enumerate(seeds):
+        eng.attack_run(n_gen, P, n_off, s, ref, 0.05, 0)
+        eng.attack_population(g, None)
+        eng.decode(g, x)
+        oc.run(ceng, mlp, xi, x, 1, obj, bad)
+        o = obj.cpu().numpy()
+        assert not bad.any().item()
+        r = np.stack([calc._objective_respected(o[b]) for b in range(B)])
+        resp[k] = r.any(axis=1)
+        if first is None:
+            first = (g.cpu().numpy(), o)
+    return p, X, resp, first
+
+
+def _t_bound(a, b, conf=0.99):
+    """Two-sample pooled-variance t half-width for the difference of the seed means."""
+    from scipy import stats
+
+    na, nb = a.shape[0], b.shape[0]
+    sp2 = ((na - 1) * a.var(axis=0, ddof=1) + (nb - 1) * b.var(axis=0, ddof=1)) / (na + nb - 2)
+    return stats.t.ppf(0.5 + conf / 2, na + nb - 2) * np.sqrt(sp2 * (1.0 / na + 1.0 / nb))
+
+
+@pytest.mark.parametrize("fixture", ["e2e_botnet_rq1_seeds.npz", "e2e_lcld_rq1_g100_seeds.npz"])
+def test_success_rate_distribution(fixture):
+    """north_star: "the constrained attack success rate must fall within +-1 pp of the
+    reference on the same initial states and budgets ... the RNG differs".  The reference
+    side is the numpy-order oracle (numpy summation orders, np.power; the closest
+    restatement of the reference's arithmetic) at >= 4 seeds (tests/golden/
+    make_e2e_seeds.py); the device runs the same states and budget at 32 other seeds.  For
+    every o_k the seed means must agree within 1 pp, or within the 99 % two-sample t
+    interval of their difference when that is wider (printed)."""
+    path = os.path.join(GOLD, fixture)
+    if not os.path.exists(path):
+        pytest.skip(f"{fixture} not generated (tests/golden/make_e2e_seeds.py)")
+    d = np.load(path, allow_pickle=False)
+    name = str(d["project"])
+    B, G = int(d["n_states"]), int(d["n_gen"])
+    thr, eps = float(d["thr"]), float(d["eps"])
+    p, X, resp, (g0, o0) = _device_seed_rates(name, B, G, int(d["n_pop"]),
+                                              int(d["n_offsprings"]), eps, thr, DEVICE_SEEDS)
+    # the device scoring agrees with the oracle's ObjectiveCalculator restatement
+    sc, mn = p.ml
+    for b in range(0, B, max(1, B // 16)):
+        x_f = mo.genetic_to_ml(p.lay, g0[b], X[b])
+        ob = mo.objectives_calc(X[b], x_f, p.constraints, p.types, sc, mn, p.weights,
+                                p.biases, 1, sc, mn, 2)
+        assert np.array_equal(mo.objectives_respected(ob, thr, eps).any(axis=0), resp[0, b])
+        np.testing.assert_allclose(o0[b], ob, rtol=1e-5, atol=1e-9)
+    sr_dev = resp.mean(axis=1)  # (S_dev, 7)
+    sr_ref = np.asarray(d["success_rate"], np.float64)  # (S_ref, 7)
+    assert sr_ref.shape[0] >= 4
+    diff = sr_dev.mean(axis=0) - sr_ref.mean(axis=0)
+    half = _t_bound(sr_dev, sr_ref)
+    bar = np.maximum(0.01, half)
+    np.set_printoptions(linewidth=200)
+    print(f"\n{fixture}: {sr_ref.shape[0]} oracle seeds, {sr_dev.shape[0]} device seeds")
+    print("  oracle o1..o7 mean", np.round(sr_ref.mean(axis=0), 4), "sd",
+          np.round(sr_ref.std(axis=0, ddof=1), 4))
+    print("  device o1..o7 mean", np.round(sr_dev.mean(axis=0), 4), "sd",
+          np.round(sr_dev.std(axis=0, ddof=1), 4))
+    print("  diff", np.round(diff, 4), "99% t half-width", np.round(half, 4))
+    print("  oracle per seed o7", np.round(sr_ref[:, 6], 4))
+    print("  device per seed o7", np.round(sr_dev[:, 6], 4))
+    assert np.all(np.abs(diff) <= bar + 1e-12), (diff, bar)
+
+
 @pytest.mark.parametrize("fixture", ["e2e_botnet_rq1.npz", "e2e_lcld_rq1_g100.npz",
                                      "e2e_lcld_rq1_g1000.npz"])
 def test_success_rate_within_1pp_at_full_config(fixture):

@@ -803,35 +803,47 @@ def test_hosted_constraints_plugin_default_problem():
 def test_hosted_plugins_attack(which):
     """Moeva2.generate with a host plugin (constraints without a device program, or a model
     with only predict_proba) runs the host-driven loop around the device calls: it tracks
-    the all-device attack (same draws; only the host columns' rounding differs) and its
-    final objectives are the plugin's own values."""
+    the all-device attack (same draws; only the host columns' rounding differs), its final
+    objectives are the plugin's own values, and with save_history="full" the history's G
+    columns are the plugin's clamped ``evaluate`` (default_problem.py:93-97, 137-140)."""
     from moeva2_amd.attacks.moeva2.classifier import Classifier
     from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
 
     p = Project("lcld")
-    B, G = 8, 4
+    B, G, P, O = 8, 4, 203, 100
     X = p.x[:B]
     model = os.path.join(RES, PROJECTS["lcld"][1])
     host = Moeva2(model, _host_lcld_constraints() if which == "constraints"
                   else make_constraints("lcld"), ml_scaler=make_scaler("lcld"), norm=2,
-                  n_gen=G, n_pop=200, n_offsprings=100, seed=4)
+                  n_gen=G, n_pop=200, n_offsprings=O, seed=4, save_history="full")
     if which == "classifier":
         host._classifier = Classifier(_NumpyMLP("lcld"))
     dev = Moeva2(model, make_constraints("lcld"), ml_scaler=make_scaler("lcld"), norm=2,
-                 n_gen=G, n_pop=200, n_offsprings=100, seed=4)
-    gh, Fh, _ = host.generate(X, 1, return_device=True)
-    gd, Fd, _ = dev.generate(X, 1, return_device=True)
-    gh, Fh, gd, Fd = (t.cpu().numpy() for t in (gh, Fh, gd, Fd))
+                 n_gen=G, n_pop=200, n_offsprings=O, seed=4, save_history="full")
+    gh, Fh, Hh = host.generate(X, 1, return_device=True)
+    gd, Fd, Hd = dev.generate(X, 1, return_device=True)
+    gh, Fh, gd, Fd, Hh, Hd = (t.cpu().numpy() for t in (gh, Fh, gd, Fd, Hh, Hd))
+    assert Hh.shape == Hd.shape == (B, P + (G - 1) * O, 3 + 10)
     same = [b for b in range(B) if np.array_equal(gh[b], gd[b])]
-    print(which, "identical final populations", len(same), "/", B)
+    best_h, best_d = Fh[:, :, 0].min(axis=1), Fd[:, :, 0].min(axis=1)
+    print(which, "identical final populations", len(same), "/", B, "mean best f1 host",
+          best_h.mean(), "device", best_d.mean())
     assert len(same) >= B // 2
+    # every state, diverged or not, reaches the same progress
+    assert abs(best_h.mean() - best_d.mean()) <= 0.02, (best_h, best_d)
     for b in same:
         np.testing.assert_allclose(Fh[b], Fd[b], rtol=1e-5, atol=1e-12)
+        np.testing.assert_allclose(Hh[b, :, 3:], Hd[b, :, 3:], rtol=1e-12, atol=1e-12)
     for b in range(B):  # host columns are the plugin's values on the final population
         x_f = mo.genetic_to_ml(p.lay, gh[b], X[b])
         if which == "constraints":
             gg = mo.lcld_constraints(x_f)
             np.testing.assert_array_equal(Fh[b, :, 2], (gg * (gg > 0)).sum(1))
+            # history: G columns sum to f3; the initial rows are the clamped plugin G of x_init
+            np.testing.assert_array_equal(Hh[b, :, 3:].sum(1), Hh[b, :, 2])
+            x0 = mo.genetic_to_ml(p.lay, mo.initial_population(p.problem(X[b]), P), X[b])
+            g0 = mo.lcld_constraints(x0)
+            np.testing.assert_array_equal(Hh[b, :P, 3:], g0 * (g0 > 0))
         else:
             sc, mn = p.ml
             f1 = mo.mlp_predict_proba(x_f * sc + mn, p.weights, p.biases)[:, 1]
@@ -919,6 +931,84 @@ def test_objective_calculator_range_assert():
     xs[0, 1, 0] = np.nan
     with pytest.raises(AssertionError):
         calc.calculate_objectives_3d(X, xs)
+
+
+@pytest.mark.parametrize("which", ["constraints", "classifier", "both"])
+def test_objective_calculator_host_plugins(which):
+    """objective_calculator.py:44-64 scores any Constraints subclass and any predict_proba
+    model: a constraints object without a device program is evaluated by its own
+    ``evaluate``, a model that is not a Dense MLP by its own ``predict_proba``, on the host;
+    the one-hot term, CV, scaling checks and f2 stay on the device (mv_objcalc_score).
+    Objectives and success rates equal the oracle's restatement."""
+    from moeva2_amd.attacks.moeva2.classifier import Classifier
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+
+    p = Project("lcld")
+    X = p.x[:10]
+    _, g, _, _, _ = _attack("lcld", X, 5, 3, P=23, O=10)
+    genes = g.cpu().numpy()
+    xs = np.stack([mo.genetic_to_ml(p.lay, genes[b], X[b]) for b in range(X.shape[0])])
+    sc, mn = p.ml
+    cons = _host_lcld_constraints() if which in ("constraints", "both") else make_constraints("lcld")
+    clf = (Classifier(_NumpyMLP("lcld")) if which in ("classifier", "both")
+           else make_classifier("lcld"))
+    scaler = make_scaler("lcld")
+    calc = ObjectiveCalculator(clf, cons, 1, {"f1": 0.25, "f2": 0.2}, min_max_scaler=scaler,
+                               norm=2, ml_scaler=scaler)
+    _, ceng, mlp = calc._device()
+    assert (ceng is None) == (which in ("constraints", "both"))
+    assert (mlp is None) == (which in ("classifier", "both"))
+    obj = calc.calculate_objectives_3d(X, xs)
+
+    def fn(xi, x):
+        return mo.objectives_calc(xi, x, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, 2)
+
+    for b in range(X.shape[0]):
+        _check_obj(obj[b], fn(X[b], xs[b]))
+    np.testing.assert_array_equal(calc.success_rate_3d(X, xs),
+                                  mo.success_rate_3d(X, xs, fn, 0.25, 0.2))
+    bad = xs.copy()
+    bad[1, 2, int(np.argmax(sc))] = (2.0 - mn[int(np.argmax(sc))]) / sc[int(np.argmax(sc))]
+    with pytest.raises(AssertionError):
+        calc.calculate_objectives_3d(X, bad)
+
+
+def test_moeva_driver_hosted_plugins(tmp_path, monkeypatch):
+    """04_moeva.py end to end with host plugins: the attack (host-driven loop) and its
+    success scoring (ObjectiveCalculator host fallback) run on a Constraints subclass
+    without a device program and a predict_proba-only model; the metrics equal the oracle's
+    success rates of the saved x_attacks."""
+    import json
+
+    from moeva2_amd.attacks.moeva2 import moeva2 as mv2
+    from moeva2_amd.config_parser.config_parser import get_config, get_dict_hash
+    from moeva2_amd.experiments.united import moeva_run
+
+    monkeypatch.setattr(moeva_run, "_constraints", lambda *a, **k: _host_lcld_constraints())
+    monkeypatch.setattr(moeva_run, "load_model", lambda path: _NumpyMLP("lcld"))
+    monkeypatch.setattr(mv2, "load_model", lambda path: _NumpyMLP("lcld"))
+    cfg_dir = os.path.join(os.path.dirname(RES), "config")
+    c = get_config(["-c", f"{cfg_dir}/moeva.yaml", "-c", f"{cfg_dir}/rq1.lcld.static.yaml",
+                    "-p", "seed=7", "-p", "budget=4", "-p", "n_initial_state=5",
+                    "-p", f"dirs.results={tmp_path}", "-j", '{"eps_list":[0.2,0.4]}'])
+    h = get_dict_hash(c)
+    m = moeva_run.run(c, verbose=False)
+    xa = np.load(tmp_path / f"x_attacks_moeva_{h}.npy")
+    assert xa.shape == (5, 203, 47)
+    on_disk = json.load(open(tmp_path / f"metrics_moeva_{h}.json"))
+    p = Project("lcld")
+    sc, mn = p.ml
+
+    def fn(xi, x):
+        return mo.objectives_calc(xi, x, p.constraints, p.types, sc, mn, p.weights, p.biases,
+                                  1, sc, mn, 2)
+
+    for k, eps in enumerate((0.2, 0.4)):
+        sr = mo.success_rate_3d(p.x[:5], xa, fn, 0.25, eps)
+        np.testing.assert_array_equal([on_disk["objectives_list"][k][f"o{i}"]
+                                       for i in range(1, 8)], sr)
+        assert m["objectives_list"][k] == on_disk["objectives_list"][k]
 
 
 def test_moeva_driver_outputs(tmp_path):

@@ -1,7 +1,9 @@
 """The engine's shipped energy reference directions (resources/ref_dirs/, used for
 get_reference_directions("energy", 3, n_pop, seed=1) at
-/root/reference/src/attacks/moeva2/moeva2.py:113) against the properties of pymoo's Riesz
-s-energy method, restated in oracle/ref_dirs_pymoo.py.  pymoo is not vendored, so the point
+/root/reference/src/attacks/moeva2/moeva2.py:113): they are exactly the product generator's
+output (moeva2_amd.attacks.moeva2.ref_dirs.riesz_energy_dirs, pymoo's Riesz s-energy method),
+and they have the properties of that method as independently restated in
+oracle/ref_dirs_pymoo.py.  pymoo is not vendored, so the point
 set itself is parity-unpinned; these tests pin the method's measurable outcomes: points on
 the simplex, the corners kept, a Riesz energy (d = 2 n_dim) within 2 % of the restated
 method's optimum and well below its starting point and uniform random points, and the
@@ -61,6 +63,36 @@ def test_shipped_dirs_vs_riesz_energy_method(restated, n):
     # uniform design: spacing and covering radius comparable to the restated method's
     assert _min_dist(X) >= 0.6 * _min_dist(R)
     assert _cover_radius(X, rng) <= 1.5 * _cover_radius(R, rng)
+
+
+@pytest.mark.parametrize("n", [200, 640])
+def test_shipped_dirs_are_the_generator_output(n):
+    """resources/ref_dirs/energy_3_{n}_seed1.npy == riesz_energy_dirs(3, n, seed=1)."""
+    from moeva2_amd.attacks.moeva2 import ref_dirs as rd
+
+    X = np.load(f"{rd._RES}/energy_3_{n}_seed1.npy", allow_pickle=False)
+    np.testing.assert_array_equal(X, rd.riesz_energy_dirs(3, n, seed=1))
+
+
+def test_generator_projection_and_energy_gradient():
+    """The generator's simplex projection against the oracle's, and its log-energy gradient
+    against central differences."""
+    from moeva2_amd.attacks.moeva2 import ref_dirs as rd
+
+    rng = np.random.default_rng(5)
+    Y = rng.normal(size=(200, 3)) * 2
+    np.testing.assert_allclose(rd.simplex_projection(Y), rp._project_simplex_rows(Y),
+                               atol=1e-15)
+    X = rng.dirichlet(np.ones(3), size=12)
+    e, g = rd.log_energy_and_grad(X, 6.0)
+    assert abs(e - rp.riesz_log_energy(X, 6.0)) < 1e-12
+    h = 1e-6
+    for i, k in ((0, 0), (5, 2), (11, 1)):
+        Xp, Xm = X.copy(), X.copy()
+        Xp[i, k] += h
+        Xm[i, k] -= h
+        num = (rd.log_energy_and_grad(Xp, 6.0)[0] - rd.log_energy_and_grad(Xm, 6.0)[0]) / (2 * h)
+        assert abs(num - g[i, k]) <= 1e-5 * max(1.0, abs(num))
 
 
 def test_restated_method_steps_stay_on_simplex():
