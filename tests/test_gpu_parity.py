@@ -189,7 +189,7 @@ def test_wide_mlp_config_matches_fp32_reference():
         np.testing.assert_allclose(F[b, :, 1:], ref[:, 1:], rtol=1e-12, atol=1e-15)
     from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
 
-    ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_iter=200)
+    ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_max_iter=200)
     outs = []
     for _ in range(2):
         eng.attack_run(4, 23, 10, 3, ref_dirs, 0.05, 0)
@@ -288,7 +288,7 @@ def test_bf16_mode_classifier(wide):
         assert worst < 0.05
         from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
 
-        ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_iter=200)
+        ref_dirs = riesz_energy_dirs(3, 20, seed=1, n_max_iter=200)
         eng.attack_run(5, 23, 10, 3, ref_dirs, 0.05, 0)
         g = torch.empty((X.shape[0], 23, p.lay.V), dtype=torch.float64, device="cuda")
         Fa = torch.empty((X.shape[0], 23, 3), dtype=torch.float64, device="cuda")
@@ -535,7 +535,7 @@ def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto", crossover="tw
 def mo_ref_dirs(n):
     from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
 
-    return riesz_energy_dirs(3, n, seed=1, n_iter=200)
+    return riesz_energy_dirs(3, n, seed=1, n_max_iter=200)
 
 
 @pytest.mark.parametrize("name,B,P,O,G,hist,cx", [
