@@ -18,7 +18,7 @@ multi-GPU: states are independent (moeva2.py:194-205).  Every step runs
          ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--shard]
-                    [--mode auto|chain|whole] [--crossover two_point|sbx]
+                    [--crossover two_point|sbx] [--mlp-dtype fp32|bf16]
 """
 import argparse
 import json
@@ -236,8 +236,9 @@ def main():
                     help="state groups (streams) of the timed attack; default: engine's choice. "
                          "--groups 1 makes every launch cover all states, like the roofline "
                          "pass, so rocprofv3 averages compare 1:1 with the bench's event times")
-    ap.add_argument("--mode", default="auto", choices=["auto", "chain", "whole"],
-                    help="attack schedule: per-phase kernel chain or one whole-attack launch")
+    ap.add_argument("--mode", default="auto", choices=["auto", "chain"],
+                    help="attack schedule (the per-phase kernel chain; the whole-attack "
+                         "kernel was retired)")
     ap.add_argument("--crossover", default="two_point", choices=["two_point", "sbx"])
     ap.add_argument("--mlp-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="classifier precision: fp32 (parity, default) or the bf16 perf mode "
@@ -348,7 +349,7 @@ def main():
     eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
-    att_ms, whole = eng.attack_time()
+    whole = False
     eng.set_profiling(False)
     rows = B * O
     Dm = int(eng.prog.mut_feats.shape[0])
@@ -390,15 +391,7 @@ def main():
                 "frac": gbs / HBM_PEAK_GBS, "traffic": traffic.get(key), "kernel": name,
                 "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": ms}
 
-    if whole:
-        n_launch_evals = B * evals_per_state
-        kernels = {"k_attack": hbm("k_attack (whole attack: one launch, one workgroup per "
-                                   "state)", eval_bytes * n_launch_evals, att_ms, "k_attack")}
-        kernels["k_attack"]["mfma_tflops"] = exec_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
-        kernels["k_attack"]["mfma_tflops_algorithmic"] = \
-            eval_flops * n_launch_evals / (att_ms * 1e-3) / 1e12
-        per_gen = {"k_attack_ms_per_attack": att_ms, "dominant": "k_attack"}
-    else:
+    if True:
         ng = max(kt["generations"], 1)
         gen_ms = kt["gen_ms"] / ng
         cons_ms = kt["cons_ms"] / ng
@@ -468,7 +461,7 @@ def main():
                    "classifier_dtype": ("bf16 perf mode (bf16 MFMA, fp32 accumulate; not a "
                                         "parity result)" if bf16 else "f32 (MFMA)"),
                    "crossover": args.crossover,
-                   "schedule": "whole-attack kernel" if whole else "per-phase kernel chain",
+                   "schedule": "per-phase kernel chain",
                    "parallelism": par},
         "attack_wall_clock_per_1k_states_s": elapsed / args.steps / states_total * 1000.0,
         "load_s": load_s,

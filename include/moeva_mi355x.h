@@ -206,8 +206,8 @@ typedef struct mv_attack_params {
  * k_survive per generation, state groups on up to 4 streams) and, for the shipped problem
  * layouts, ONE launch (k_attack: one workgroup per state runs every generation). */
 int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
-/* 0: auto (default; currently the chain), 1: per-phase kernel chain, 2: whole-attack kernel
- * when the problem layout has an instance (else the chain). */
+/* 0: auto (default), 1: per-phase kernel chain -- the same schedule.  2 (the retired
+ * whole-attack kernel, measured slower than the chain) is rejected with MV_ERR_ARG. */
 int mv_set_attack_mode(mv_engine* e, int32_t mode);
 /* Classifier precision of the engine's fitness path (mv_evaluate, mv_attack_run): 0 = fp32
  * (default; the parity mode: exact fp32 products on v_mfma_f32_16x16x4f32, as Keras computes
@@ -215,8 +215,7 @@ int mv_set_attack_mode(mv_engine* e, int32_t mode);
  * bf16, fp32 accumulation on v_mfma_f32_16x16x32_bf16; f1 is no longer Keras's value, so
  * results are not parity results).  No reference counterpart: an engine option. */
 int mv_set_mlp_precision(mv_engine* e, int32_t bf16);
-/* Device ms of the last profiled mv_attack_run's k_attack launch (0 if the chain ran) and
- * whether the last run was the whole-attack kernel. */
+/* Kept for ABI stability: the whole-attack kernel was retired, so *ms = 0 and *whole = 0. */
 int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);
 /* Final population: genes dev [B][P][V], F dev [B][P][3] (either may be NULL). */
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);

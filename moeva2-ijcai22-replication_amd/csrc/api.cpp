@@ -135,9 +135,7 @@ struct mv_engine {
   // profiling
   int cx_kind = 0;          // 0: two-point (reference), 1: SBX
   double sbx_eta = 30.0, cx_prob = 0.9;
-  int attack_mode = 0;      // 0: auto, 1: per-phase chain, 2: whole-attack kernel
-  bool last_whole = false;  // the last mv_attack_run used the whole-attack kernel
-  hipEvent_t ev_att[2] = {};
+  int attack_mode = 0;      // 0: auto, 1: per-phase chain (the only schedule)
   bool profiling = false;
   std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
   int n_var_rec = 0, n_surv_rec = 0;
@@ -167,8 +165,6 @@ struct mv_engine {
     }
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
-    for (auto e : ev_att)
-      if (e) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
 };
@@ -697,90 +693,6 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   HIPCHK(hipGetLastError());
   HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
   HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
-  // attack mode: 2 = whole-attack kernel, 1 = per-phase chain, 0 = auto (the chain: measured
-  // faster on every BASELINE config so far); MV_ATTACK=whole|chain overrides
-  const char* env_mode = std::getenv("MV_ATTACK");
-  int mode = e->attack_mode;
-  if (env_mode && std::strcmp(env_mode, "whole") == 0) mode = 2;
-  if (env_mode && std::strcmp(env_mode, "chain") == 0) mode = 1;
-  // (the whole-attack kernel's classifier phase is fp32 only: the bf16 mode runs the chain)
-  e->last_whole = mode == 2 && !e->mlp_bf16 && attack_supported(e->p, P, O, R);
-  if (e->last_whole) {
-    // the whole GA loop in one launch: one workgroup per state (attack.hip)
-    AttackArgs A{};
-    A.ev = base_rows(e);
-    A.ev.n = P;
-    A.ev.total = B * P;
-    A.ev.mode = 0;
-    A.ev.genes_in = e->pool;
-    A.ev.in_rows = S;
-    A.ev.out_rows = S;
-    A.ev.F = e->poolF;
-    A.ev.hist = prm->history ? e->hist : nullptr;
-    A.ev.hist_rows = hist_rows;
-    A.ev.hist_w = hist_w;
-    A.ev.xml = e->xml;
-    A.ev.xml_rows = P > O ? P : O;  // states run different phases at the same time
-    A.va = base_rows(e);
-    A.va.n = O;
-    A.va.total = B * O;
-    A.va.mode = 1;
-    A.va.genes_in = e->pool;
-    A.va.in_rows = S;
-    A.va.parents = e->parents;
-    A.va.genes_out = e->pool;
-    A.va.out_rows = S;
-    A.va.out_map = e->free_slot;
-    A.va.F = e->poolF;
-    A.va.hist = prm->history ? e->hist : nullptr;
-    A.va.hist_rows = hist_rows;
-    A.va.hist_w = hist_w;
-    A.va.seed = prm->seed;
-    A.va.xml = e->xml;
-    A.va.xml_rows = P > O ? P : O;
-    SurvArgs& s = A.sa;
-    s.n_survive = P;
-    s.P = P;
-    s.O = O;
-    s.F = e->poolF;
-    s.S = S;
-    s.pop_slot = e->pop_slot;
-    s.free_slot = e->free_slot;
-    s.pop_slot_out = e->pop_slot;
-    s.ref = e->ref;
-    s.R = R;
-    s.mu = prm->mu;
-    s.seed = prm->seed;
-    s.ideal = e->ideal;
-    s.worst = e->worst;
-    s.extreme = e->extreme;
-    s.has_extreme = e->has_ext;
-    s.O_next = O;
-    s.dom_g = e->dom_g;
-    s.dom_stride = e->dom_stride;
-    A.parents = e->parents;
-    A.B = B;
-    A.P = P;
-    A.O = O;
-    A.G = G;
-    if (std::getenv("MV_ATT_PROF")) {  // development aid: per-phase clock64 sums per state
-      if (!e->d_phase) {
-        HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 16 * sizeof(long long)));
-        e->attack_allocs.push_back(e->d_phase);
-      }
-      A.prof = e->d_phase;
-    }
-    if (e->profiling) {
-      for (auto& ev : e->ev_att)
-        if (!ev) HIPCHK(hipEventCreate(&ev));
-      HIPCHK(hipEventRecord(e->ev_att[0], stream));
-    }
-    HIPCHK(launch_attack(A, stream));
-    if (e->profiling) HIPCHK(hipEventRecord(e->ev_att[1], stream));
-    e->n_var_rec = 0;
-    e->n_surv_rec = 0;
-    return MV_OK;
-  }
   // Initial states are independent: split them into state groups, each running its own
   // generation chain on its own stream, so one group's latency-bound survival overlaps the
   // other groups' throughput-bound kernels.  Results do not depend on the grouping (every
@@ -837,7 +749,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     s.extreme += b0 * 9;
     s.has_extreme += b0;
     if (s.parents_out) s.parents_out += b0 * O;
-    if (s.phase) s.phase += b0 * 16;
+    if (s.phase) s.phase += b0 * 32;
     if (s.dom_g) s.dom_g += b0 * s.dom_stride;
     return s;
   };
@@ -875,7 +787,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.dom_stride = e->dom_stride;
   if (std::getenv("MV_SURV_PHASES")) {
     if (!e->d_phase) {
-      HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 16 * sizeof(long long)));
+      HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 32 * sizeof(long long)));
       e->attack_allocs.push_back(e->d_phase);
     }
     sa.phase = e->d_phase;
@@ -923,8 +835,6 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     HIPCHK(stage_rows(vq[q], gs[q], &slot_va[q]));
   }
   sa.N = P + O;
-  const bool rows_fused = std::getenv("MV_ROWS_FUSED") && e->cx_kind == 0 &&
-                          rows_fused_lds(e->p) <= 160 * 1024;
   for (int g = 1; g < G; ++g) {
     const int hist_row0 = P + (g - 1) * O;
     sa.gen = g;
@@ -934,14 +844,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       hipStream_t st = gs[q];
       const bool prof = e->profiling && q == 0;
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
-      if (rows_fused) {  // development A/B: k_gen + k_cons as one k_rows launch
-        HIPCHK(launch_rows_fused(vq[q], slot_va[q], g, hist_row0, st));
-        if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
-      } else {
-        HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
-        if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
-        HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
-      }
+      HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
+      if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+      HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
       HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
       if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));
@@ -981,17 +886,25 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
   if (survive_ms) *survive_ms = ts;
   if (n_generations) *n_generations = e->n_var_rec < e->n_surv_rec ? e->n_var_rec : e->n_surv_rec;
   if (e->d_phase && e->B > 0) {  // development aid: survival phase split of the last generation
-    std::vector<long long> ph((size_t)e->B * 16);
+    std::vector<long long> ph((size_t)e->B * 32);
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(ph.data(), e->d_phase, ph.size() * sizeof(long long), hipMemcpyDeviceToHost));
-    double acc[16] = {0};
+    double acc[32] = {0};
     for (int b = 0; b < e->B; ++b)
-      for (int k = 1; k < 10; ++k) acc[k] += (double)(ph[(size_t)b * 16 + k] - ph[(size_t)b * 16 + k - 1]);
+      for (int k = 1; k < 10; ++k) acc[k] += (double)(ph[(size_t)b * 32 + k] - ph[(size_t)b * 32 + k - 1]);
     std::fprintf(stderr, "[mv] survival phase cycles (mean over %d states):", e->B);
     for (int k = 1; k < 10; ++k) std::fprintf(stderr, " p%d=%.0f", k, acc[k] / e->B);
+    // sub-phase marks (cycles since phase 0): 21/22 extremes (ASF loop, combine), 16..20
+    // niching (keys, member lists, ranks, levels, round keys)
+    std::fprintf(stderr, " | t:");
+    for (int k : {3, 21, 22, 4, 5, 10, 6, 16, 17, 18, 19, 20, 7}) {
+      double t = 0.0;
+      for (int b = 0; b < e->B; ++b) t += (double)(ph[(size_t)b * 32 + k] - ph[(size_t)b * 32]);
+      std::fprintf(stderr, " %d=%.0f", k, t / e->B);
+    }
     double red = 0.0, afast = 0.0, nflag = 0.0;
     for (int b = 0; b < e->B; ++b) {
-      const long long* q = &ph[(size_t)b * 16];
+      const long long* q = &ph[(size_t)b * 32];
       red += (double)(q[11] - q[1]);
       afast += (double)(q[10] - q[5]);
       nflag += (double)q[12];
@@ -1020,38 +933,17 @@ int mv_set_mlp_precision(mv_engine* e, int32_t bf16) {
 }
 
 int mv_set_attack_mode(mv_engine* e, int32_t mode) {
-  if (!e || mode < 0 || mode > 2)
-    return fail(MV_ERR_ARG, "attack mode must be 0 (auto), 1 (chain) or 2 (whole)");
+  if (!e || mode < 0 || mode > 1)
+    return fail(MV_ERR_ARG, "attack mode must be 0 (auto) or 1 (chain); the whole-attack "
+                            "kernel (2) was retired: it measured slower than the chain");
   e->attack_mode = mode;
   return MV_OK;
 }
 
 int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole) {
   if (!e) return fail(MV_ERR_ARG, "null engine");
-  if (whole) *whole = e->last_whole ? 1 : 0;
-  if (ms) {
-    *ms = 0.0;
-    if (e->last_whole && e->ev_att[1]) {
-      float t = 0.f;
-      HIPCHK(hipEventSynchronize(e->ev_att[1]));
-      HIPCHK(hipEventElapsedTime(&t, e->ev_att[0], e->ev_att[1]));
-      *ms = t;
-    }
-  }
-  if (e->last_whole && e->d_phase && std::getenv("MV_ATT_PROF") && e->B > 0) {
-    std::vector<long long> ph((size_t)e->B * 16);
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(ph.data(), e->d_phase, (size_t)e->B * 4 * sizeof(long long),
-                     hipMemcpyDeviceToHost));
-    double acc[4] = {0, 0, 0, 0};
-    for (int b = 0; b < e->B; ++b)
-      for (int k = 0; k < 4; ++k) acc[k] += (double)ph[(size_t)b * 4 + k];
-    const double g = e->n_gen > 0 ? e->n_gen : 1;
-    std::fprintf(stderr,
-                 "[mv] k_attack cycles per state-generation: rows %.0f mlp %.0f survive %.0f "
-                 "all %.0f\n", acc[0] / e->B / g, acc[1] / e->B / g, acc[2] / e->B / g,
-                 acc[3] / e->B / g);
-  }
+  if (whole) *whole = 0;
+  if (ms) *ms = 0.0;
   return MV_OK;
 }
 

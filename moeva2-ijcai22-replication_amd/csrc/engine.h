@@ -133,7 +133,6 @@ struct RowsArgs {
   double sbx_eta;           // SBX distribution index (30)
   int do_eval;              // 0: variation only
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
-  int xml_rows;             // whole-attack kernel: xml rows per state (0: n)
 };
 
 // Survival ------------------------------------------------------------------------------
@@ -170,21 +169,6 @@ struct SurvArgs {
   long long* phase;         // [B][16] clock64() at phase boundaries (development), or NULL
   unsigned long long* dom_g;  // N > SURV_NLDS: dominance bitsets [B][dom_stride] in HBM
   size_t dom_stride;
-};
-
-// Whole attack in one launch (attack.hip) -----------------------------------------------
-#ifndef MV_ATT_T
-#define MV_ATT_T 256
-#endif
-constexpr int ATT_T = MV_ATT_T;  // threads per whole-attack workgroup (two workgroups per CU)
-constexpr int ATT_SLOTS = 8;    // constant-memory argument slots per device
-struct AttackArgs {
-  RowsArgs ev;              // initial evaluation: mode 0, n = P, pool slots 0..P-1
-  RowsArgs va;              // offspring: mode 1, n = O, out_map = free slots
-  SurvArgs sa;              // survival, slot mode (N / gen / parents passed per generation)
-  int* parents;             // [B][O/2][2] tournament output (slots)
-  int B, P, O, G;
-  long long* prof;          // [B][4] clock64 sums per phase (rows, mlp, survive, all) or NULL
 };
 
 // Stand-alone classifier forward (Classifier.predict_proba) -------------------------------

@@ -29,7 +29,6 @@
 #include "narrow.h"
 #include "philox.h"
 #include "rowops.h"
-#include "rows_fused.h"
 #include "wave.h"
 
 namespace mv {
@@ -189,10 +188,9 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
 // SBX: the SBX crossover option compiled in (a separate instance: its pow()-heavy path
 // doubled the two-point kernel's registers, halving its occupancy).
 template <bool IDENT, int NT, bool SBX>
-__global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
+__device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
+                                         unsigned char* smem) {
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk(a.n, rows_wg, wave);
@@ -392,15 +390,20 @@ __global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0
   }
 }
 
+template <bool IDENT, int NT, bool SBX>
+__global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0, int rows_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gen_rows<IDENT, NT, SBX>(c_rows[slot], gen, hist_row0, rows_wg, smem);
+}
+
 // k_cons: the constraint program of each evaluated row (Constraints.evaluate numpy path +
 // default_problem.py:93-97,128-129) -> f3 (+ G / history columns).  One workgroup = one
 // state x a chunk of its rows, as k_gen; the row's genes (written by k_gen) are scattered
 // into the wave's ML row buffer whose immutable features were written once, then each lane
 // evaluates its (register-packed) ops.
 template <bool FULL, bool IDENT, int NT>
-__global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int rows_wg) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const RowsArgs& a = c_rows[slot];
+__device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int rows_wg,
+                                          unsigned char* smem) {
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
@@ -492,18 +495,29 @@ __global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int ro
   }
 }
 
-// k_rows: k_gen + k_cons fused (rows_fused.h): one workgroup = one state x a chunk of its
-// rows; each child row is read (parents) and written once, its constraints evaluated from
-// the wave's LDS row right after the variation -- no re-read of the child genes.
-template <bool IDENT, int NT, bool FULL>
-__global__ __launch_bounds__(VARY_T) void k_rows(int slot, int gen, int hist_row0, int rows_wg) {
+template <bool FULL, bool IDENT, int NT>
+__global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int rows_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  cons_rows<FULL, IDENT, NT>(c_rows[slot], hist_row0, rows_wg, smem);
+}
+
+// k_genc: k_gen and k_cons as two phases of ONE launch over the same row chunks (each wave
+// evaluates the constraints of the rows it generated).  Phase 2 reads the children back
+// from L2 (written a few microseconds earlier by the same workgroup) instead of HBM, and
+// the chain loses a launch boundary; the phases run one after the other, so the kernel
+// needs the larger of the two register and LDS footprints, not their sum (the fused row
+// loop of round 2, k_rows, kept both phases' registers live: 208 VGPRs).
+template <bool IDENT, int NT, bool SBX>
+__global__ __launch_bounds__(VARY_T) void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
+  static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
-  const int nchunk = (a.n + rows_wg - 1) / rows_wg;
-  const int id = xcd_local_id();
-  const int b = id / nchunk;
-  const int r0 = (id - b * nchunk) * rows_wg;
-  rows_state<IDENT, NT, FULL, VARY_T>(a, b, gen, hist_row0, r0, min(a.n, r0 + rows_wg), smem);
+  gen_rows<IDENT, NT, SBX>(a, gen, hist_row0, rows_wg, smem);
+  // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
+  // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  cons_rows<false, IDENT, NT>(a, hist_row0, rows_wg, smem);
 }
 
 // k_narrow: k_gen + k_cons for narrow rows, one lane per row (narrow.h).
@@ -1487,9 +1501,48 @@ static hipError_t launch_narrow(const RowsArgs& a, int slot, int gen, int hist_r
 #undef NG
 }
 
+// k_genc (k_gen + k_cons in one launch) for the wave-per-row evaluation of IDENT problems
+// without the LCLD financial ops (the botnet shape).  MV_GENC=0 keeps the two launches.
+static bool use_genc(const RowsArgs& a) {
+  const char* s = std::getenv("MV_GENC");  // read per launch: tests flip it in-process
+  const int nt = vary_nt(a.p);
+  return !(s && s[0] == '0') && a.do_eval && a.p.ident && !a.p.full_ops && !use_narrow(a) &&
+         (nt == 4 || nt == 8 || nt == 16);
+}
+
+template <int NT>
+static hipError_t genc_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw,
+                          bool sbx) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_genc<true, NT, false>);
+    allow_lds(k_genc<true, NT, true>);
+    configured = true;
+  }
+  if (sbx)
+    hipLaunchKernelGGL((k_genc<true, NT, true>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  else
+    hipLaunchKernelGGL((k_genc<true, NT, false>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+  return hipGetLastError();
+}
+
 hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
   if (use_narrow(a)) return launch_narrow(a, slot, gen, hist_row0, stream);
+  if (use_genc(a)) {
+    const int B = a.total / a.n;
+    const int rw = vary_rows_per_wg(a.n);
+    const dim3 grid(B * ((a.n + rw - 1) / rw));
+    const int nt = vary_nt(a.p);
+    const VaryOff o = vary_offsets(a.p);
+    const size_t lg = gen_lds(o, gen_regc(a.p, nt), true, true).total;
+    const size_t lc = cons_lds_total(o);
+    const size_t lds = lg > lc ? lg : lc;
+    const bool sbx = a.mode == 1 && a.cx_kind == 1;
+    if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    if (nt == 8) return genc_go<8>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    return genc_go<16>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+  }
   const int B = a.total / a.n;
   const int rw = vary_rows_per_wg(a.n);
   const dim3 grid(B * ((a.n + rw - 1) / rw));
@@ -1516,6 +1569,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
 hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || !a.do_eval) return hipSuccess;
   if (use_narrow(a)) return hipSuccess;  // done by k_narrow in launch_gen
+  if (use_genc(a)) return hipSuccess;    // done by k_genc in launch_gen
   const int B = a.total / a.n;
   const int rw = vary_rows_per_wg(a.n);
   const dim3 grid(B * ((a.n + rw - 1) / rw));
@@ -1544,59 +1598,9 @@ hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t s
 #undef CONS
 }
 
-template <bool IDENT, int NT, bool FULL>
-static hipError_t rows_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw) {
-  static bool configured = false;
-  if (!configured) {
-    allow_lds(k_rows<IDENT, NT, FULL>);
-    configured = true;
-  }
-  hipLaunchKernelGGL((k_rows<IDENT, NT, FULL>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
-  return hipGetLastError();
-}
-
-size_t rows_fused_lds(const DProblem& p) { return fused_lds(vary_offsets(p), VARY_T / 64).total; }
-
-hipError_t launch_rows_fused(const RowsArgs& a, int slot, int gen, int hist_row0,
-                             hipStream_t stream) {
-  if (a.total <= 0) return hipSuccess;
-  const int B = a.total / a.n;
-  const int rw = vary_rows_per_wg(a.n);
-  const dim3 grid(B * ((a.n + rw - 1) / rw));
-  const int nt = vary_nt(a.p);
-  const size_t lds = rows_fused_lds(a.p);
-#define RW(I, N, F) return rows_go<I, N, F>(grid, lds, stream, slot, gen, hist_row0, rw)
-  if (a.p.ident) {
-    if (nt == 1) RW(true, 1, false);
-    if (nt == 2) RW(true, 2, false);
-    if (nt == 4) RW(true, 4, false);
-    if (nt == 8) RW(true, 8, false);
-    RW(true, 16, false);
-  }
-  if (a.p.full_ops) {
-    if (nt == 1) RW(false, 1, true);
-    if (nt == 2) RW(false, 2, true);
-    if (nt == 4) RW(false, 4, true);
-    if (nt == 8) RW(false, 8, true);
-    RW(false, 16, true);
-  }
-  if (nt == 1) RW(false, 1, false);
-  if (nt == 2) RW(false, 2, false);
-  if (nt == 4) RW(false, 4, false);
-  if (nt == 8) RW(false, 8, false);
-  RW(false, 16, false);
-#undef RW
-}
-
-// Variation + evaluation of the rows in the per-phase chain: k_gen then k_cons.  (The fused
-// k_rows was measured slower here -- 2 workgroups per CU instead of 4 hide less of the
-// per-row latency -- and with several state-group streams it showed rare run-to-run
-// differences that were not found; it is kept for MV_ROWS_FUSED experiments only.  Its body
-// is the whole-attack kernel's row phase, which is deterministic and tested.)
+// Variation + evaluation of the rows in the per-phase chain: k_gen then k_cons.
 hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream) {
-  if (a.do_eval && rows_fused_lds(a.p) <= 160 * 1024 && std::getenv("MV_ROWS_FUSED"))
-    return launch_rows_fused(a, slot, gen, hist_row0, stream);
   hipError_t e = launch_gen(a, slot, gen, hist_row0, stream);
   if (e != hipSuccess) return e;
   return launch_cons(a, slot, hist_row0, stream);

@@ -115,28 +115,6 @@ __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + CONS_W * o.rb;
 }
 
-// fused row kernel (k_rows, whole-attack rows phase): regions A, B, C, E, then one D-wide
-// row per wave
-struct FusedLds {
-  unsigned a_at, b_at, c_at, e_at, rows_at, total;
-};
-__host__ __device__ inline FusedLds fused_lds(const VaryOff& o, int waves) {
-  FusedLds l{};
-  unsigned at = 0;
-  l.a_at = at;
-  at += o.a_end;
-  l.b_at = at;
-  at += o.b_end - o.b_at;
-  l.c_at = at;
-  at += o.vb - o.c_at;
-  l.e_at = at;
-  at += o.sb - o.e_at;
-  l.rows_at = at;
-  at += waves * o.rb;
-  l.total = at;
-  return l;
-}
-
 // k_predict: TR-row tiles (32, or 16 for inputs too wide for a 32-row tile)
 __host__ __device__ inline size_t predict_region1_bytes(int D4, int hmax, int TR) {
   const size_t a = (size_t)TR * (D4 + 1) * sizeof(float);
@@ -152,9 +130,6 @@ __host__ __device__ inline size_t predict_lds_bytes(int D4, int hmax, int Klast,
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
 hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, const double* genes,
                          double* x, hipStream_t stream);
-size_t attack_lds_bytes(const DProblem& p, int P, int O, int R, int T);
-bool attack_supported(const DProblem& p, int P, int O, int R);
-hipError_t launch_attack(const AttackArgs& args, hipStream_t stream);
 
 // Launch-argument ring (constant memory, per device): stage a copy on `stream`, launch with
 // the returned slot, then release it on the same stream after the slot's last launch.
@@ -169,10 +144,6 @@ hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream);
 hipError_t launch_rows(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream);
-// k_rows: k_gen + k_cons fused (rows_fused.h); rows_fused_lds: its LDS bytes
-hipError_t launch_rows_fused(const RowsArgs& a, int slot, int gen, int hist_row0,
-                             hipStream_t stream);
-size_t rows_fused_lds(const DProblem& p);
 hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double* x,
                               double* G, hipStream_t stream);
 hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,

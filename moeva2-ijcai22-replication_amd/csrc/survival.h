@@ -84,7 +84,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
 #define TAKE(field, bytes)        \
   o.field = off;                  \
   off = (unsigned)align16(off + (size_t)(bytes));
-  TAKE(F, (size_t)N * 3 * 8)
+  TAKE(F, (size_t)NW * 64 * 3 * 8)  // rows past N hold NaN (dominance padding)
   TAKE(ref, (size_t)R * 3 * 8)
   TAKE(U, (size_t)RN * 3 * 8)
   TAKE(Uf, (size_t)RN * 16)
@@ -191,6 +191,13 @@ __device__ __forceinline__ int block_scan_excl(int* v, int n, int* wsum) {
     __syncthreads();
   }
   return carry;
+}
+
+// v_min_f32 without the NaN canonicalisation the compiler adds for fminf (finite operands)
+__device__ __forceinline__ float vmin_f32(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 __device__ __forceinline__ double wred_min(double v) {
@@ -331,7 +338,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   const double pre_worst = tid < 3 ? a.worst[(size_t)b * 3 + tid] : 0.0;
   const bool slot_mode = a.pop_slot != nullptr;
 #define PHASE(k) \
-  if (a.phase && tid == 0) a.phase[(size_t)b * 16 + (k)] = clock64();
+  if (a.phase && tid == 0) a.phase[(size_t)b * 32 + (k)] = clock64();
   PHASE(0)
 
   // ---- load merged F, ref points
@@ -351,8 +358,14 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     L.front_of[m] = -1;
     L.sel[m] = 0;
   }
+  for (int m = N + tid; m < NW * 64; m += T) {  // padding rows: compare false both ways
+    L.F[m * 3 + 0] = __builtin_nan("");
+    L.F[m * 3 + 1] = __builtin_nan("");
+    L.F[m * 3 + 2] = __builtin_nan("");
+  }
   for (int r = tid; r < R * 3; r += T) L.ref[r] = a.ref[r];
   if (tid < 9) pext[tid] = a.extreme[(size_t)b * 9 + tid];
+  if (tid == 0) L.iscal[14] = 0;  // dominance work counter
   for (int q = tid; q < NW; q += T) {
     L.ranked[q] = 0ull;
     L.cur[q] = 0ull;
@@ -360,14 +373,11 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   __syncthreads();
   PHASE(1)
 
-  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: one
-  // wave, while the other waves start the dominance pass below (independent of it; its
-  // results are first read after the pass's barrier).  min/max of these values do not
-  // depend on the reduction order (NaN propagates either way; no -0.0 objective exists:
-  // f1 is a probability, f2 a sqrt, f3 a sum starting at +0.0).  Above SURV_NLDS (HBM
-  // bitsets, N^2 work 10x the headline's) the dominance pass keeps every wave: ideal/worst
-  // first, then a barrier.
-  const bool iw_overlap = N <= SURV_NLDS;
+  // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: wave
+  // 0, before it joins the dominance pass below (independent of it; its results are first
+  // read after the pass's barrier).  min/max of these values do not depend on the reduction
+  // order (NaN propagates either way; no -0.0 objective exists: f1 is a probability, f2 a
+  // sqrt, f3 a sum starting at +0.0).
   if (wave == 0) {
     double mn[3], mx[3], wp[3];
     for (int k = 0; k < 3; ++k) {
@@ -410,59 +420,50 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       wpop[k] = vwp;
     }
   }
-  if (!iw_overlap) __syncthreads();
   PHASE(11)
 
-  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the
-  // unordered 64x64 block pairs (qi <= qj) split into two 32-row halves of block qj; lane
-  // l holds row i = 64 qi + l (NaN past N: dominates nothing).  One pass of the six
-  // compares per (i, j) gives both directions: lt && !gt -> i dominates j (ballot = word qi
-  // of dom[j]); gt && !lt -> j dominates i, gathered per lane into the 32-bit half h of word
-  // qj of dom[i] (off-diagonal pairs only; the diagonal block is covered by its ballots).
+  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the unordered
+  // 64x64 block pairs (qi <= qj) split into the four 16-row quarters of block qj, taken
+  // from an LDS counter (wave 0 joins after ideal/worst).  Lane l holds row i = 64 qi + l;
+  // the 16 rows j of the quarter are LDS broadcasts, fully unrolled (F is padded to whole
+  // blocks with NaN rows, which compare false both ways: no bounds tests).  One pass of
+  // the six compares per (i, j) gives both directions: lt && !gt -> i dominates j (the
+  // ballot is word qi of dom[j], kept by lane u); gt && !lt -> j dominates
+  // i, bit u of this lane's 16-bit quarter qq of word qj of dom[i] (off-diagonal pairs
+  // only: the diagonal block is covered by its ballots).
   {
-    unsigned* dom32 = (unsigned*)L.dom;
-    const int n_items = NW * (NW + 1);
-    const int w0 = iw_overlap ? 1 : 0;  // first dominance wave (wave 0: ideal/worst)
-    for (int t = wave - w0; wave >= w0 && t < n_items; t += T / 64 - w0) {
-      const int h = t & 1;
-      int qi = 0, rem = t >> 1;
+    unsigned short* dom16 = (unsigned short*)L.dom;
+    const int n_q = NW * (NW + 1) * 2;  // block pairs x 4 quarters
+    for (;;) {
+      int t = 0;
+      if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
+      t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+      if (t >= n_q) break;
+      const int qq = t & 3;
+      int qi = 0, rem = t >> 2;
       while (rem >= NW - qi) {
         rem -= NW - qi;
         ++qi;
       }
       const int qj = qi + rem;
       const int i = qi * 64 + lane;
-      const bool ok = i < N;
-      const double fi0 = ok ? L.F[i * 3 + 0] : __builtin_nan("");
-      const double fi1 = ok ? L.F[i * 3 + 1] : __builtin_nan("");
-      const double fi2 = ok ? L.F[i * 3 + 2] : __builtin_nan("");
-      const int j0 = qj * 64 + h * 32;
-      const int jn = min(32, N - j0);
-      // four independent rows per step (the step is latency-bound: LDS broadcast ->
-      // compares -> ballot); lane jj keeps the ballot of row j0 + jj until the item ends
-      unsigned acc = 0u;
+      const double fi0 = L.F[i * 3 + 0], fi1 = L.F[i * 3 + 1], fi2 = L.F[i * 3 + 2];
+      const int j0 = qj * 64 + qq * 16;
+      const double* fj = L.F + j0 * 3;
       unsigned long long mine = 0ull;
-      for (int jj = 0; jj < jn; jj += 4) {
-        double g[4][3];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = min(j0 + jj + u, N - 1);
-          g[u][0] = L.F[j * 3];
-          g[u][1] = L.F[j * 3 + 1];
-          g[u][2] = L.F[j * 3 + 2];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const bool valid = jj + u < jn;
-          const bool lt = (fi0 < g[u][0]) | (fi1 < g[u][1]) | (fi2 < g[u][2]);
-          const bool gt = (fi0 > g[u][0]) | (fi1 > g[u][1]) | (fi2 > g[u][2]);
-          const unsigned long long m = __ballot(valid && lt && !gt);
-          if (lane == jj + u) mine = m;
-          acc |= (valid && gt && !lt) ? (1u << ((jj + u) & 31)) : 0u;
-        }
+      unsigned acc = 0u;
+#pragma unroll 4
+      for (int u = 0; u < 16; ++u) {
+        const double g0 = fj[u * 3], g1 = fj[u * 3 + 1], g2 = fj[u * 3 + 2];
+        const bool lt = (fi0 < g0) | (fi1 < g1) | (fi2 < g2);
+        const bool gt = (fi0 > g0) | (fi1 > g1) | (fi2 > g2);
+        const unsigned long long m = __ballot(lt && !gt);
+        mine = lane == u ? m : mine;
+        acc |= (gt && !lt) ? (1u << u) : 0u;
       }
-      if (lane < jn) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
-      if (qi != qj && ok) dom32[((size_t)i * NW + qj) * 2 + h] = acc;
+      if (lane < 16 && j0 + lane < N)
+        L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
+      if (qi != qj && i < N) dom16[((size_t)i * NW + qj) * 4 + qq] = (unsigned short)acc;
     }
   }
   __syncthreads();
@@ -578,6 +579,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         }
       }
     }
+    PHASE(21)
     for (int i = 0; i < 3; ++i) {
       wave_argbest(bv[i], bi[i], [](double v, int i1, double w, int i2) {
         return arg_better(v, i1, w, i2);
@@ -621,6 +623,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     }
     __syncthreads();
+    PHASE(22)
     if (tid == 0) {
       // nadir (get_nadir_point with the call-site argument swap)
       double M[3][3], plane[3] = {1.0, 1.0, 1.0};
@@ -711,10 +714,12 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     // the halves combine with lane swaps: fp32 minimum (exact), then the fp64 candidate
     // minimum in np.argmin's order (arg_better is a total order, so the combination equals
     // the sequential scan).
-    const int jmid = RN / 2;
+    const int nh = RN >> 1;  // directions per half (wave-uniform loop counts); an odd RN's
+                             // last direction goes to the second half's chain 0
     for (int v = tid; v < 2 * n_ranked; v += T) {
       const int p = v >> 1, hf = v & 1;
-      const int jlo = hf ? jmid : 0, jhi = hf ? RN : jmid;
+      const int jb = hf ? nh : 0;
+      const bool odd = hf && (RN & 1);
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
@@ -740,15 +745,24 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         }
         continue;
       }
-      float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;  // 4 independent chains
-      int j = jlo;
-      for (; j + 4 <= jhi; j += 4) {
-        b0 = fminf(b0, d2f(j));
-        b1 = fminf(b1, d2f(j + 1));
-        b2 = fminf(b2, d2f(j + 2));
-        b3 = fminf(b3, d2f(j + 3));
+      // 4 independent min chains over the half's directions jb + 4k + u (chain 0 also takes
+      // the tail); v_min_f32 directly (fminf would re-canonicalise the chain every step).
+      // With |N|^2 finite every d is finite (|u| = 1); otherwise the chains stay +inf and
+      // the individual takes the exact pass below.
+      float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;
+      const int n4 = nh >> 2;
+      if (nn < __builtin_inff()) {
+#pragma unroll 2
+        for (int k = 0; k < n4; ++k) {
+          const int j = jb + 4 * k;
+          b0 = vmin_f32(b0, d2f(j));
+          b1 = vmin_f32(b1, d2f(j + 1));
+          b2 = vmin_f32(b2, d2f(j + 2));
+          b3 = vmin_f32(b3, d2f(j + 3));
+        }
+        for (int j = jb + 4 * n4; j < jb + nh; ++j) b0 = vmin_f32(b0, d2f(j));
+        if (odd) b0 = vmin_f32(b0, d2f(RN - 1));
       }
-      for (; j < jhi; ++j) b0 = fminf(b0, d2f(j));
       float best = fminf(fminf(b0, b1), fminf(b2, b3));
       best = fminf(best, __shfl_xor(best, 1, 64));
       const float lim = best + 3e-5f * (nn + best);
@@ -766,31 +780,50 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
           }
         };
         // second sweep only over the chains whose minimum is within lim (usually just the
-        // chain holding the minimum): chain u = jlo + u + 4k, chain 0 also takes the tail.
-        // d2f is the same expression as in the first sweep, so no candidate is missed, and
-        // arg_better is a total order, so the visiting order does not change the result.
-        const int n4 = (jhi - jlo) >> 2;
+        // chain holding the minimum).  d2f is the same expression as in the first sweep, so
+        // no candidate is missed, and arg_better is a total order, so the visiting order
+        // does not change the result.
         unsigned cm = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) | (b2 <= lim ? 4u : 0u) |
                       (b3 <= lim ? 8u : 0u);
+        // collect the candidate indices first (cheap selects, so the lanes' hits at
+        // different steps cost little), then evaluate them in a wave-uniform loop: calling
+        // the fp64 distance inside the sweep ran it once per step at which ANY lane had a hit
+        int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
+        auto hit = [&](int jc) {
+          c0 = nc == 0 ? jc : c0;
+          c1 = nc == 1 ? jc : c1;
+          c2 = nc == 2 ? jc : c2;
+          c3 = nc == 3 ? jc : c3;
+          ++nc;
+        };
         while (cm) {
           const int u = __builtin_ctz(cm);
           cm &= cm - 1u;
           int k = 0;
           for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
-            const int jc = jlo + 4 * k + u;
+            const int jc = jb + 4 * k + u;
             const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
-            if (d0 <= lim) cand(jc);
-            if (d1 <= lim) cand(jc + 4);
-            if (d2 <= lim) cand(jc + 8);
-            if (d3 <= lim) cand(jc + 12);
+            if (d0 <= lim) hit(jc);
+            if (d1 <= lim) hit(jc + 4);
+            if (d2 <= lim) hit(jc + 8);
+            if (d3 <= lim) hit(jc + 12);
           }
           for (; k < n4; ++k) {
-            const int jc = jlo + 4 * k + u;
-            if (d2f(jc) <= lim) cand(jc);
+            const int jc = jb + 4 * k + u;
+            if (d2f(jc) <= lim) hit(jc);
           }
-          if (u == 0)
-            for (int jc = jlo + 4 * n4; jc < jhi; ++jc)
-              if (d2f(jc) <= lim) cand(jc);
+          if (u == 0) {
+            for (int jc = jb + 4 * n4; jc < jb + nh; ++jc)
+              if (d2f(jc) <= lim) hit(jc);
+            if (odd && d2f(RN - 1) <= lim) hit(RN - 1);
+          }
+        }
+        const bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;  // rare: the full exact pass
+        if (!ovf) {
+          if (nc > 0) cand(c0);
+          if (nc > 1) cand(c1);
+          if (nc > 2) cand(c2);
+          if (nc > 3) cand(c3);
         }
         const double od = __shfl_xor(bd, 1, 64);
         const int oj = __shfl_xor(bj, 1, 64);
@@ -799,8 +832,12 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
           bj = oj;
         }
         if (!hf) {
-          L.niche[p] = bj;
-          L.dist[p] = bd;
+          if (ovf) {
+            L.key[atomicAdd(&L.iscal[15], 1)] = p;
+          } else {
+            L.niche[p] = bj;
+            L.dist[p] = bd;
+          }
         }
       } else if (!hf) {
         L.key[atomicAdd(&L.iscal[15], 1)] = p;
@@ -810,7 +847,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     PHASE(10)
     // exact np.argmin over sqrt'ed distances for the flagged individuals
     const int n_flag = L.iscal[15];
-    if (a.phase && tid == 0) a.phase[(size_t)b * 16 + 12] = n_flag;
+    if (a.phase && tid == 0) a.phase[(size_t)b * 32 + 12] = n_flag;
     for (int t = tid; t < n_flag; t += T) {
       const int p = L.key[t];
       const int m = L.I[p];
@@ -879,6 +916,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       sk[p] = ((unsigned long long)nich[p] << 42) | ((unsigned long long)key << 10) | (unsigned)p;
     }
     __syncthreads();
+    PHASE(16)
     for (int p = tid; p < Lc; p += T) {
       const int np_ = nich[p];
       if (cnt[np_] == 0)
@@ -892,6 +930,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       mem[start[np_] + atomicAdd(&fill[np_], 1)] = p;
     }
     __syncthreads();
+    PHASE(17)
     // grank = rank of sk[p] among all keys = members of smaller niches (start) + rank inside
     // its own niche, counted over that niche's members only
     for (int p = tid; p < Lc; p += T) {
@@ -910,6 +949,10 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         atomicMin(&bestkr[np_], r);
     }
     __syncthreads();
+    PHASE(18)
+    // level of each pick; per level its member count (high half-word) and non-empty flag
+    // (bit 0), so ONE exclusive scan gives every level's first bucket position and its round
+    // index (the number of non-empty levels before it)
     for (int p = tid; p < Lc; p += T) {
       const int np_ = nich[p];
       const int kr = grank[p] - start[np_];
@@ -917,26 +960,41 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       if (cnt[np_] == 0) j = kr == bestkr[np_] ? 0 : kr + (kr < bestkr[np_] ? 1 : 0);
       const int l = cnt[np_] + j;
       lev[p] = l;
-      L.lround[l] = 1;  // level is non-empty
+      grank[p] = atomicAdd(&L.lround[l], 1 << 16) >> 16;  // position inside the level
+      atomicOr(&L.lround[l], 1);
     }
     __syncthreads();
-    block_scan_excl<T>(L.lround, nlev, wsum);  // rounds before each level
+    PHASE(19)
+    block_scan_excl<T>(L.lround, nlev, wsum);
     // output order: ascending (level, round key of the niche, niche); a niche picks at most
-    // once per level, so a pick's rank is its position among the remaining slots
+    // once per level, so a pick's rank is the members of lower levels plus its rank by
+    // (round key, niche) inside its own level -- counted over that level's bucket only, and
+    // only for levels that start below n_rem
+    int* bucket = L.key;  // [Lc] last-front members grouped by level
     for (int p = tid; p < Lc; p += T) {
       const int l = lev[p];
-      const unsigned kr = rng.draw((uint32_t)(L.lround[l] * RN + nich[p]), (uint32_t)gen,
+      const int lr = L.lround[l];
+      const unsigned kr = rng.draw((uint32_t)((lr & 0xFFFF) * RN + nich[p]), (uint32_t)gen,
                                    TAG_NICHE_PERM).x;
-      // (level, round key, niche) is unique per member (a niche picks at most once per
-      // level), so no position field is needed: niche 11 bits, round key 32, level 21
-      sk[p] = ((unsigned long long)l << 43) | ((unsigned long long)kr << 11) |
-              (unsigned long long)nich[p];
+      sk[p] = ((unsigned long long)kr << 11) | (unsigned long long)nich[p];
+      bucket[(lr >> 16) + grank[p]] = p;
     }
     __syncthreads();
+    PHASE(20)
     for (int p = tid; p < Lc; p += T) {
+      const int l = lev[p];
+      const int b0 = L.lround[l] >> 16;
+      if (b0 >= n_rem) continue;
+      const int b1 = l + 1 < nlev ? (L.lround[l + 1] >> 16) : Lc;
       const unsigned long long kp = sk[p];
-      int r = 0;
-      for (int q = 0; q < Lc; ++q) r += sk[q] < kp ? 1 : 0;
+      int r = b0;
+      int t = b0;
+      for (; t + 4 <= b1; t += 4) {
+        const int m0 = bucket[t], m1 = bucket[t + 1], m2 = bucket[t + 2], m3 = bucket[t + 3];
+        r += (sk[m0] < kp ? 1 : 0) + (sk[m1] < kp ? 1 : 0) + (sk[m2] < kp ? 1 : 0) +
+             (sk[m3] < kp ? 1 : 0);
+      }
+      for (; t < b1; ++t) r += sk[bucket[t]] < kp ? 1 : 0;
       if (r < n_rem) L.surv[until + r] = fs + p;
     }
     for (int p = tid; p < until; p += T) L.surv[p] = p;

@@ -329,16 +329,13 @@ class Engine:
         self.mlp_dtype = dtype
 
     def set_attack_mode(self, mode: str):
-        """"chain": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per
-        generation); "whole": one k_attack launch for the whole attack (one workgroup per
-        state) when the problem layout has an instance; "auto" (default): the faster one."""
-        check(lib().mv_set_attack_mode(self._h, {"auto": 0, "chain": 1, "whole": 2}[mode]))
-
-    def attack_time(self):
-        """(device ms of the last profiled whole-attack launch, whether it ran as one launch)."""
-        ms, whole = C.c_double(), C.c_int32()
-        check(lib().mv_get_attack_time(self._h, C.byref(ms), C.byref(whole)))
-        return ms.value, bool(whole.value)
+        """"chain"/"auto": the per-phase kernel chain (k_gen, k_cons, k_mlp2, k_survive per
+        generation), the engine's only schedule.  The whole-attack kernel ("whole") was
+        retired (measured slower)."""
+        if mode not in ("auto", "chain"):
+            raise ValueError(f"attack mode {mode!r}: 'auto' or 'chain' (the whole-attack "
+                             "kernel was retired)")
+        check(lib().mv_set_attack_mode(self._h, {"auto": 0, "chain": 1}[mode]))
 
     def kernel_times(self):
         """Summed device ms of k_vary / k_mlp / k_survive over the last profiled attack."""

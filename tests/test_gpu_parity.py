@@ -504,7 +504,7 @@ def test_variation_vs_oracle(name, kind):
             np.all(got <= np.stack(gus)[:, None] + 1e-9)
 
 
-# ------------------------------------------------------------------ whole attack
+# ------------------------------------------------------------------ attack chain
 def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto", crossover="two_point",
             norm=2):
     from moeva2_amd.problem import get_engine
@@ -543,20 +543,21 @@ def mo_ref_dirs(n):
     ("lcld", 37, 203, 100, 7, 2, "two_point"), ("lcld_augmented", 11, 43, 20, 6, 1, "two_point"),
     ("lcld", 3, 643, 320, 3, 0, "two_point"), ("botnet", 5, 43, 20, 6, 1, "sbx"),
     ("lcld", 9, 43, 20, 6, 2, "sbx")])
-def test_whole_attack_kernel_matches_phase_chain(name, B, P, O, G, hist, cx):
-    """The one-launch attack (k_attack: one workgroup per state runs every generation) is
-    bit-identical to the per-phase chain (k_gen, k_cons, k_mlp2, k_survive per generation):
-    final genes, objectives and the whole history."""
+def test_attack_chain_deterministic(name, B, P, O, G, hist, cx, monkeypatch):
+    """Two runs of the per-phase chain (k_gen, k_cons, k_mlp2, k_survive per generation) give
+    bit-identical genes, objectives and history, with 1 and 4 state groups; the retired
+    whole-attack schedule is rejected."""
     X = Project(name).x[:B]
-    e1, g1, F1, h1, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="whole", crossover=cx)
-    _, whole = e1.attack_time()
-    assert whole, "the shipped layout must run as one launch"
-    e2, g2, F2, h2, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="chain", crossover=cx)
-    assert not e2.attack_time()[1]
+    monkeypatch.setenv("MV_GROUPS", "1")
+    e1, g1, F1, h1, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="chain", crossover=cx)
+    monkeypatch.setenv("MV_GROUPS", "4")
+    _, g2, F2, h2, _ = _attack(name, X, G, 13, hist=hist, P=P, O=O, mode="auto", crossover=cx)
     np.testing.assert_array_equal(g1.cpu().numpy(), g2.cpu().numpy())
     np.testing.assert_array_equal(F1.cpu().numpy(), F2.cpu().numpy())
     if hist:
         np.testing.assert_array_equal(h1.cpu().numpy(), h2.cpu().numpy())
+    with pytest.raises(ValueError):
+        e1.set_attack_mode("whole")
 
 
 @pytest.mark.parametrize("name,B,P,O,G,hist,norm", [
