@@ -211,17 +211,21 @@ def data_note(w, B):
     return f"{src[w['project']]} ({how}) + {clf} and shipped scaler"
 
 
-def load_traffic(workload, whole):
+PROFILE_ROUNDS = ("r03", "r02")  # newest first: traffic measured on the current kernels wins
+
+
+def load_traffic(workload):
     """Per-kernel HBM bytes per launch from the committed rocprofv3 PMC passes of `workload`
-    under the schedule that actually ran (`whole`: one-launch attack, else the kernel chain);
-    {} when that workload/schedule was never measured."""
-    path = os.path.join(ROOT, "profiles", "r02",
-                        f"pmc_traffic_{workload}_{'whole' if whole else 'chain'}.json")
-    if not os.path.exists(path):
-        return {}
-    with open(path) as fh:
-        return {k: v["traffic_bytes"] for k, v in json.load(fh).items()
-                if isinstance(v, dict) and "traffic_bytes" in v}
+    (the per-phase kernel chain, the only schedule), newest profile round first; {} when that
+    workload was never measured.  A kernel the current code no longer launches simply finds
+    no entry (e.g. k_gen/k_cons of round 2 once k_genc replaced them)."""
+    for rnd in PROFILE_ROUNDS:
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_traffic_{workload}_chain.json")
+        if os.path.exists(path):
+            with open(path) as fh:
+                return {k: v["traffic_bytes"] for k, v in json.load(fh).items()
+                        if isinstance(v, dict) and "traffic_bytes" in v}
+    return {}
 
 
 def main():
@@ -349,7 +353,6 @@ def main():
     eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
-    whole = False
     eng.set_profiling(False)
     rows = B * O
     Dm = int(eng.prog.mut_feats.shape[0])
@@ -383,7 +386,7 @@ def main():
     # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
     if args.crossover == "two_point" and not bf16:
-        traffic = load_traffic(args.workload, whole)
+        traffic = load_traffic(args.workload)
 
     def hbm(name, bytes_launch, ms, key):
         gbs = bytes_launch / (ms * 1e-3) / 1e9
@@ -419,20 +422,30 @@ def main():
         }
         per_gen = {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
         # LCLD-shaped rows run k_narrow (csrc/narrow.h narrow_ok): variation + decode + f2 +
-        # constraint program in ONE launch timed as "k_gen"; the "k_cons" events then bracket
-        # an empty step, so the pair is reported as one kernel with the combined bytes
-        # (parents read + child written + ML row + f2/f3 + history columns per row)
-        narrow = (V <= 32 and Dm4 <= 64 and prog.C <= 64 and not (prog.op_code == 3).any()
-                  and args.crossover == "two_point" and os.environ.get("MV_NARROW") != "0")
-        if narrow:
+        # constraint program in ONE launch; IDENT wave-per-row problems (the botnet shape) run
+        # k_genc (k_gen and k_cons as two phases of one launch).  Either way the engine's
+        # "k_gen" events bracket the one launch and its "k_cons" events an empty step, so the
+        # pair is reported as one kernel with the combined algorithmic bytes.
+        rk = kt.get("row_kernel", "k_gen+k_cons")
+        if rk == "k_narrow":
             hist_b = {"full": 8 * (3 + prog.C), "reduced": 24}.get(w["history"], 0)
             nb = 2 * V * 8 + Dm4 * 4 + 16 + hist_b
             kernels.pop("k_gen")
             kernels.pop("k_cons")
             kernels["k_narrow"] = hbm("k_narrow (crossover + mutation + ML row + distance + "
                                       "constraint program, one lane per row)", nb * rows,
-                                      gen_ms + cons_ms, "k_gen")
+                                      gen_ms + cons_ms, "k_narrow")
             per_gen = {"k_narrow": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+        elif rk == "k_genc":
+            # parents read + child written once (2*V*8) + f2 + f3; phase 2 re-reads the child
+            # rows its own workgroup just wrote (L2/MALL hits, not algorithmic HBM bytes)
+            nb = gen_bytes + 8
+            kernels.pop("k_gen")
+            kernels.pop("k_cons")
+            kernels["k_genc"] = hbm("k_genc (crossover + mutation + distance, then the "
+                                    "constraint program over the same rows; one launch)",
+                                    nb * rows, gen_ms + cons_ms, "k_genc")
+            per_gen = {"k_genc": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
         per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
     dom = per_gen["dominant"]
     if args.shard:

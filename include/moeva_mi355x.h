@@ -230,6 +230,11 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
  * (constraints + f3), ms[2] k_mlp (classifier, f1), ms[3] k_survive (survival + next
  * tournament), summed over the profiled generations. */
 int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
+/* The kernels an attack generation runs for its offspring rows under the engine's current
+ * options: 0 = k_gen then k_cons, 1 = k_narrow (one lane per row, both in one launch; the
+ * k_cons events then bracket nothing), 2 = k_genc (k_gen and k_cons as two phases of one
+ * launch; likewise).  Lets a profiler attribute ms[0] + ms[1] of mv_get_phase_times. */
+int mv_get_row_kernel(mv_engine* e, int32_t* kind);
 
 /* The engine's pow for the variation operators (host build of csrc/detmath.h det_pow, the
  * same IEEE operation sequence as the device code): out[i] = det_pow(x[i], y[i]) for host

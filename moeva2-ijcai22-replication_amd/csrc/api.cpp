@@ -863,6 +863,16 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   return MV_OK;
 }
 
+int mv_get_row_kernel(mv_engine* e, int32_t* kind) {
+  if (!e || !kind) return fail(MV_ERR_ARG, "null argument");
+  RowsArgs a = base_rows(e);
+  a.n = 2;
+  a.total = 2;
+  a.mode = 1;
+  *kind = row_kernel_kind(a);
+  return MV_OK;
+}
+
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations) {
   if (!e) return fail(MV_ERR_ARG, "null engine");

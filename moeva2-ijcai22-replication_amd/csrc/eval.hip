@@ -663,7 +663,7 @@ __device__ __forceinline__ void dense_mfma_bf(const float* __restrict__ in, int 
 }
 
 // Final Dense + softmax for row t (one thread), weights staged in LDS: ws[k*nout + c], wsb[c].
-// fp32 logits, softmax in fp64 rounded to fp32 (softmax_pick).
+// fp32 logits, Keras's fp32 softmax (rowops.h softmax_e).
 __device__ __forceinline__ void last_layer_softmax(const float* in, int ldi, int K, int nout,
                                                    const float* ws, const float* wsb, int t,
                                                    float (&prob)[8]) {
@@ -1503,11 +1503,18 @@ static hipError_t launch_narrow(const RowsArgs& a, int slot, int gen, int hist_r
 
 // k_genc (k_gen + k_cons in one launch) for the wave-per-row evaluation of IDENT problems
 // without the LCLD financial ops (the botnet shape).  MV_GENC=0 keeps the two launches.
+// k_genc's genes per lane: the exact ceil(max(V, Dm4) / 64) from 4 to 8 (every unused
+// register slot costs a masked instruction per row in every phase), else 16.
+static int genc_nt(const DProblem& p) {
+  const int m = p.V > p.Dm4 ? p.V : p.Dm4;
+  const int nt = (m + 63) / 64;
+  return nt <= 4 ? 4 : nt <= 8 ? nt : 16;
+}
+
 static bool use_genc(const RowsArgs& a) {
   const char* s = std::getenv("MV_GENC");  // read per launch: tests flip it in-process
-  const int nt = vary_nt(a.p);
   return !(s && s[0] == '0') && a.do_eval && a.p.ident && !a.p.full_ops && !use_narrow(a) &&
-         (nt == 4 || nt == 8 || nt == 16);
+         (a.p.V > a.p.Dm4 ? a.p.V : a.p.Dm4) > 128;
 }
 
 template <int NT>
@@ -1526,6 +1533,12 @@ static hipError_t genc_go(dim3 grid, size_t lds, hipStream_t s, int slot, int ge
   return hipGetLastError();
 }
 
+int row_kernel_kind(const RowsArgs& a) {
+  if (use_narrow(a)) return 1;
+  if (use_genc(a)) return 2;
+  return 0;
+}
+
 hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream) {
   if (a.total <= 0) return hipSuccess;
   if (use_narrow(a)) return launch_narrow(a, slot, gen, hist_row0, stream);
@@ -1533,13 +1546,16 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const int B = a.total / a.n;
     const int rw = vary_rows_per_wg(a.n);
     const dim3 grid(B * ((a.n + rw - 1) / rw));
-    const int nt = vary_nt(a.p);
+    const int nt = genc_nt(a.p);
     const VaryOff o = vary_offsets(a.p);
     const size_t lg = gen_lds(o, gen_regc(a.p, nt), true, true).total;
     const size_t lc = cons_lds_total(o);
     const size_t lds = lg > lc ? lg : lc;
     const bool sbx = a.mode == 1 && a.cx_kind == 1;
     if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    if (nt == 5) return genc_go<5>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    if (nt == 6) return genc_go<6>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    if (nt == 7) return genc_go<7>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
     if (nt == 8) return genc_go<8>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
     return genc_go<16>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
   }

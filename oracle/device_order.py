@@ -15,8 +15,9 @@ and the device attack can be compared trajectory for trajectory:
   first layer's bias by an fmaf chain in feature order (k_setup_states); the Dense layers
   as v_mfma_f32_16x16x4f32 accumulations (each output an fmaf chain over k in the order
   16 kg + 4 ka + s for kg, then s = 0..3, then ka = 0..3); the last Dense layer as four
-  sequential quarters combined ((q0 + q1) + q2) + q3; the 2-way softmax in fp64 rounded
-  to fp32.  One fp32 fmaf is restated as round32(a * b + c) evaluated in fp64, where a * b
+  sequential quarters combined ((q0 + q1) + q2) + q3; Keras's fp32 softmax (h = z - max,
+  exp correctly rounded to fp32, fp32 class-order sum and division: softmax_keras32).
+  One fp32 fmaf is restated as round32(a * b + c) evaluated in fp64, where a * b
   is exact; the fp64 rounding of the sum can differ from the fused single rounding only if
   it lands exactly on an fp32 midpoint (probability ~2^-29 per operation).
 * f2: each of 64 lanes sums the squared distances of features lane + 64 t in order, the 64
@@ -225,12 +226,20 @@ def f1_device_order(prob: "mo.Problem", x_f: np.ndarray) -> np.ndarray:
             ps = _fma32(h[:, k:k + 1], W[k][None, :], ps)
         q.append(ps)
     z = ((((q[0] + q[1]) + q[2]) + q[3]) + prob.biases[nl - 1].astype(np.float32))
-    z = z.astype(np.float64)
-    e = np.exp(z - z.max(axis=1, keepdims=True))
-    den = np.zeros(z.shape[0])
+    return softmax_keras32(z)[:, prob.minimize_class].astype(np.float64)
+
+
+def softmax_keras32(z):
+    """csrc/rowops.h softmax_e: Keras's fp32 softmax of fp32 logits z (n, n_out) -- h = z - max
+    in fp32, e = exp(h) correctly rounded to fp32 (fp64 exp, one rounding), the class-order
+    fp32 sum, e / sum in fp32."""
+    z = np.asarray(z, np.float32)
+    h = (z - z.max(axis=1, keepdims=True)).astype(np.float32)
+    e = np.exp(h.astype(np.float64)).astype(np.float32)
+    den = np.zeros(z.shape[0], np.float32)
     for c in range(z.shape[1]):
-        den = den + e[:, c]
-    return (e[:, prob.minimize_class] / den).astype(np.float32).astype(np.float64)
+        den = (den + e[:, c]).astype(np.float32)
+    return (e / den[:, None]).astype(np.float32)
 
 
 def wave_tree(v):

@@ -9,11 +9,11 @@ import bench  # noqa: E402
 
 
 def test_headline_traffic_is_attached_to_the_chain_schedule():
-    t = bench.load_traffic("rq1.botnet.static", whole=False)
-    assert set(t) >= {"k_gen", "k_cons", "k_mlp", "k_survive"}
+    t = bench.load_traffic("rq1.botnet.static")
+    assert set(t) >= {"k_mlp", "k_survive"}
+    assert {"k_genc"} <= set(t) or {"k_gen", "k_cons"} <= set(t)
     assert all(v > 0 for v in t.values())
 
 
-def test_unmeasured_workload_or_schedule_gets_no_traffic():
-    assert bench.load_traffic("rq1.botnet.static", whole=True) == {}
-    assert bench.load_traffic("synthetic.botnet.wide", whole=False) == {}
+def test_unmeasured_workload_gets_no_traffic():
+    assert bench.load_traffic("synthetic.botnet.wide") == {}

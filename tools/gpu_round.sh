@@ -24,10 +24,10 @@ for s in $STEPS; do
     pmc) run pmc_fetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --n-gen 20 --groups 1 > $O/pmc_fetch.log 2>&1
          run pmc_write timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --n-gen 20 --groups 1 > $O/pmc_write.log 2>&1
          run pmc_mfma timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_mfma -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --n-gen 20 --groups 1 > $O/pmc_mfma.log 2>&1
-         mkdir -p profiles/r02
-         python3 tools/pmc_traffic.py profiles/r02/pmc_traffic_${W}_${M}.json $(find $O/pmc_fetch $O/pmc_write -name '*counter_collection.csv') > $O/pmc_traffic.log 2>&1
+         mkdir -p profiles/${ROUND:-r03}
+         python3 tools/pmc_traffic.py profiles/${ROUND:-r03}/pmc_traffic_${W}_${M}.json $(find $O/pmc_fetch $O/pmc_write -name '*counter_collection.csv') > $O/pmc_traffic.log 2>&1
          python3 tools/pmc_summary.py $(find $O/pmc_mfma -name '*counter_collection.csv') > $O/pmc_mfma.txt 2>&1
-         cp profiles/r02/pmc_traffic_${W}_${M}.json $O/ ; cat $O/pmc_traffic.log $O/pmc_mfma.txt ;;
+         cp profiles/${ROUND:-r03}/pmc_traffic_${W}_${M}.json $O/ ; cat $O/pmc_traffic.log $O/pmc_mfma.txt ;;
     bench) run bench bash -c "timeout -k 10 600 python -u bench.py $BA ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.log"
            python3 tools/show_bench.py $O/bench.json ;;
   esac

@@ -16,7 +16,8 @@ import json
 import sys
 from collections import defaultdict
 
-KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_mlp": "k_mlp2<", "k_survive": "k_survive<"}
+KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_genc": "k_genc<", "k_narrow": "k_narrow<",
+        "k_mlp": "k_mlp2<", "k_survive": "k_survive<"}
 
 
 def per_dispatch(paths, counter):
