@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <numeric>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -921,7 +922,22 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
     }
     std::fprintf(stderr, " | ideal/worst=%.0f assoc_fast=%.0f flagged=%.1f", red / e->B,
                  afast / e->B, nflag / e->B);
-    std::fprintf(stderr, "\n");
+    // the launch lasts as long as its slowest state: per-phase maxima and the total's tail
+    std::vector<double> tot(e->B);
+    double pmax[10] = {0};
+    int fmax = 0;
+    for (int b = 0; b < e->B; ++b) {
+      const long long* q = &ph[(size_t)b * 32];
+      tot[b] = (double)(q[9] - q[0]);
+      for (int k = 1; k < 10; ++k) pmax[k] = std::max(pmax[k], (double)(q[k] - q[k - 1]));
+      fmax = std::max(fmax, (int)q[12]);
+    }
+    std::sort(tot.begin(), tot.end());
+    std::fprintf(stderr, " | total mean=%.0f p50=%.0f p90=%.0f max=%.0f | phase max:",
+                 std::accumulate(tot.begin(), tot.end(), 0.0) / e->B, tot[e->B / 2],
+                 tot[(size_t)(e->B * 9 / 10)], tot.back());
+    for (int k = 1; k < 10; ++k) std::fprintf(stderr, " p%d=%.0f", k, pmax[k]);
+    std::fprintf(stderr, " flagged max=%d\n", fmax);
   }
   return MV_OK;
 }

@@ -730,7 +730,15 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       // minimum can hold the fp64 minimum: those few get the exact fp64 distance and
       // np.argmin's order (first index among equal sqrt'ed distances).  A NaN or overflow
       // sends the individual to the full exact pass below.
-      const float n0 = (float)Nn[0], n1 = (float)Nn[1], n2 = (float)Nn[2];
+      // The pre-filter runs on N scaled by a power of two (exact) to a largest component in
+      // [1, 2): argmin of the perpendicular distance is scale-invariant, and unscaled
+      // coordinates overflow / underflow fp32 whenever nadir - ideal collapses in one
+      // objective (den = 1e-12): at botnet generation 1000 that sent 72 of 303 individuals
+      // per state to the serial exact pass below.  The candidates are then evaluated exactly
+      // on the unscaled N.
+      const double amax = fmax(fabs(Nn[0]), fmax(fabs(Nn[1]), fabs(Nn[2])));
+      const double sc = amax > 0.0 && amax < __builtin_inf() ? ldexp(1.0, -ilogb(amax)) : 1.0;
+      const float n0 = (float)(Nn[0] * sc), n1 = (float)(Nn[1] * sc), n2 = (float)(Nn[2] * sc);
       const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
       auto d2f = [&](int j) {
         const float4 u = L.Uf[j];
@@ -783,8 +791,8 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         // chain holding the minimum).  d2f is the same expression as in the first sweep, so
         // no candidate is missed, and arg_better is a total order, so the visiting order
         // does not change the result.
-        unsigned cm = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) | (b2 <= lim ? 4u : 0u) |
-                      (b3 <= lim ? 8u : 0u);
+        const unsigned cm0 = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) |
+                             (b2 <= lim ? 4u : 0u) | (b3 <= lim ? 8u : 0u);
         // collect the candidate indices first (cheap selects, so the lanes' hits at
         // different steps cost little), then evaluate them in a wave-uniform loop: calling
         // the fp64 distance inside the sweep ran it once per step at which ANY lane had a hit
@@ -796,29 +804,60 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
           c3 = nc == 3 ? jc : c3;
           ++nc;
         };
-        while (cm) {
-          const int u = __builtin_ctz(cm);
-          cm &= cm - 1u;
-          int k = 0;
-          for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
-            const int jc = jb + 4 * k + u;
-            const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
-            if (d0 <= lim) hit(jc);
-            if (d1 <= lim) hit(jc + 4);
-            if (d2 <= lim) hit(jc + 8);
-            if (d3 <= lim) hit(jc + 12);
+        // every direction of this half whose fp32 value is within lim, in chain order
+        auto sweep = [&](auto&& on_hit) {
+          unsigned cm = cm0;
+          while (cm) {
+            const int u = __builtin_ctz(cm);
+            cm &= cm - 1u;
+            int k = 0;
+            for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
+              const int jc = jb + 4 * k + u;
+              const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
+              if (d0 <= lim) on_hit(jc);
+              if (d1 <= lim) on_hit(jc + 4);
+              if (d2 <= lim) on_hit(jc + 8);
+              if (d3 <= lim) on_hit(jc + 12);
+            }
+            for (; k < n4; ++k) {
+              const int jc = jb + 4 * k + u;
+              if (d2f(jc) <= lim) on_hit(jc);
+            }
+            if (u == 0) {
+              for (int jc = jb + 4 * n4; jc < jb + nh; ++jc)
+                if (d2f(jc) <= lim) on_hit(jc);
+              if (odd && d2f(RN - 1) <= lim) on_hit(RN - 1);
+            }
           }
-          for (; k < n4; ++k) {
-            const int jc = jb + 4 * k + u;
-            if (d2f(jc) <= lim) hit(jc);
-          }
-          if (u == 0) {
-            for (int jc = jb + 4 * n4; jc < jb + nh; ++jc)
-              if (d2f(jc) <= lim) hit(jc);
-            if (odd && d2f(RN - 1) <= lim) hit(RN - 1);
-          }
+        };
+        sweep(hit);
+        bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;
+        if (ovf) {
+          // Crowded directions (late botnet generations: nadir - ideal of f2 shrinks to ~0.017,
+          // the aspiration directions bunch up near the f2 axis and 20+ of them pass lim):
+          // refine the hits with the perpendicular vector itself, e = (n.u) u - n in fp32,
+          // which has no |n|^2 - s^2 cancellation.  Its error against the exact distance is
+          // below 8.4e-7 |n||e| + 3e-7 |e|^2 + 2e-13 |n|^2 (s: 3e-7 |n|; e: 4.2e-7 |n| +
+          // 6e-8 |e|; |e|^2: 3 roundings), so every hit within twice that (taken 2.4x
+          // larger) of the refined minimum rb -- the fp64 argmin among them -- is kept.  Both
+          // halves of the pair take the branch (ovf is symmetric), so the shuffles are safe.
+          auto d2d = [&](int j) {
+            const float4 u = L.Uf[j];
+            const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
+            const float e0 = fmaf(sp, u.x, -n0), e1 = fmaf(sp, u.y, -n1);
+            const float e2 = fmaf(sp, u.z, -n2);
+            return fmaf(e0, e0, fmaf(e1, e1, e2 * e2));
+          };
+          float rb = __builtin_inff();
+          sweep([&](int jc) { rb = fminf(rb, d2d(jc)); });
+          rb = fminf(rb, __shfl_xor(rb, 1, 64));
+          const float lr = rb + (4e-6f * sqrtf(nn) * sqrtf(rb) + 2e-6f * rb + 1e-11f * nn);
+          nc = 0;
+          sweep([&](int jc) {
+            if (d2d(jc) <= lr) hit(jc);
+          });
+          ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;  // rare: the full exact pass below
         }
-        const bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;  // rare: the full exact pass
         if (!ovf) {
           if (nc > 0) cand(c0);
           if (nc > 1) cand(c1);
@@ -845,17 +884,22 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     }
     __syncthreads();
     PHASE(10)
-    // exact np.argmin over sqrt'ed distances for the flagged individuals
+    // exact np.argmin over sqrt'ed distances for the flagged individuals: one individual per
+    // wave, the directions spread over the lanes (j = lane + 64 k), then the wave's argmin in
+    // np.argmin's order (arg_better is a total order, so the split does not change the
+    // result).  A thread-serial scan here cost 90 k cycles per state at botnet generation
+    // 1000, where the aspiration directions crowd together and 72 of 303 individuals per
+    // state have more pre-filter candidates than the fast pass keeps.
     const int n_flag = L.iscal[15];
     if (a.phase && tid == 0) a.phase[(size_t)b * 32 + 12] = n_flag;
-    for (int t = tid; t < n_flag; t += T) {
+    for (int t = wave; t < n_flag; t += T / 64) {
       const int p = L.key[t];
       const int m = L.I[p];
       double Nn[3];
       for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
       double bd = __builtin_inf();
-      int bj = 0;
-      for (int j = 0; j < RN; ++j) {
+      int bj = INT_MAX;
+      for (int j = lane; j < RN; j += 64) {
         const double* u = &L.U[j * 3];
         const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
         const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
@@ -865,8 +909,13 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
           bj = j;
         }
       }
-      L.niche[p] = bj;
-      L.dist[p] = bd;
+      wave_argbest(bd, bj, [](double v, int i1, double w, int i2) {
+        return arg_better(v, i1, w, i2);
+      });
+      if (lane == 0) {
+        L.niche[p] = bj;
+        L.dist[p] = bd;
+      }
     }
     __syncthreads();
   }

@@ -12,8 +12,8 @@ import csv
 import sys
 from collections import defaultdict
 
-KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_mlp": "k_mlp2<", "k_predict": "k_predict<",
-        "k_survive": "k_survive<", "k_attack": "k_attack", "k_rows": "k_rows<"}
+KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_genc": "k_genc<", "k_narrow": "k_narrow<",
+        "k_mlp": "k_mlp2<", "k_predict": "k_predict<", "k_survive": "k_survive<"}
 
 
 def key(name):
