@@ -13,10 +13,13 @@ The objectives are evaluated in the engine's summation orders (oracle/device_ord
 same element values as the reference restatement, the classifier / distance / constraint
 sums in the order the HIP kernels use) and the variation operators use the engine's pow
 (oracle/device_order.py:det_pow = csrc/detmath.h), so the oracle's attack and the device
-attack follow the same trajectories unless a rare fp32 double rounding flips a comparison.  The success rates of the numpy-order oracle (moeva_oracle.evaluate) at the same
-seed are kept in the fixture as ``success_rate_numpy_order`` (NUMPY_ORDER below).
+attack follow the same trajectories unless a rare fp32 double rounding flips a comparison.
+The classifier's softmax is Keras's fp32 arithmetic on both sides (csrc/rowops.h softmax_e,
+device_order.softmax_keras32).  The success rates of the numpy-order oracle
+(moeva_oracle.evaluate) at the same seed are kept in the fixture as
+``success_rate_numpy_order`` (NUMPY_ORDER below).
 
-    python tests/golden/make_e2e.py botnet_rq1     # 387 states x 1000 gens (~40 min, 8 cores)
+    python tests/golden/make_e2e.py botnet_rq1     # 387 states x 1000 gens (~60 min, 8 cores)
     python tests/golden/make_e2e.py lcld_rq1_g100   # 64 states x 100 gens
     python tests/golden/make_e2e.py lcld_rq1_g1000  # 64 states x 1000 gens
 """
