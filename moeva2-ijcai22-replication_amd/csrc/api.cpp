@@ -105,6 +105,8 @@ struct mv_engine {
   bool attack_ready = false;
   bool has_model = false;
   long long* d_phase = nullptr;  // MV_SURV_PHASES=1: survival phase clocks [B][16]
+  long long* d_gphase = nullptr; // MV_GEN_PHASES=1: k_genc clocks [grid][8] (one group)
+  size_t gphase_n = 0;
   unsigned long long* dom_g = nullptr;  // P + O > SURV_NLDS: survival dominance bitsets
   size_t dom_stride = 0;
   float* xml = nullptr;  // k_vary -> k_mlp scratch
@@ -646,6 +648,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       err = dalloc(dst, n);
       if (err == hipSuccess) e->attack_allocs.push_back((void*)*dst);
     };
+    e->d_gphase = nullptr;
+    e->gphase_n = 0;
     A(&e->pool, (size_t)B * S * V);
     A(&e->poolF, (size_t)B * S * 3);
     A(&e->pop_slot, (size_t)B * P);
@@ -829,6 +833,16 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_w = hist_w;
   va.seed = prm->seed;
   va.xml = e->xml;
+  if (std::getenv("MV_GEN_PHASES") && ngrp == 1) {  // development: k_genc phase clocks
+    const size_t n = (size_t)B * O * 8;  // >= grid * 8 (at least one row per workgroup)
+    if (e->gphase_n < n) {
+      HIPCHK(hipMalloc((void**)&e->d_gphase, n * sizeof(long long)));
+      e->attack_allocs.push_back(e->d_gphase);
+      e->gphase_n = n;
+    }
+    HIPCHK(hipMemsetAsync(e->d_gphase, 0, n * sizeof(long long), stream));
+    va.gphase = e->d_gphase;
+  }
   int slot_va[MAX_GROUPS];
   RowsArgs vq[MAX_GROUPS];
   for (int q = 0; q < ngrp; ++q) {
@@ -896,6 +910,31 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
   if (mlp_ms) *mlp_ms = tm;
   if (survive_ms) *survive_ms = ts;
   if (n_generations) *n_generations = e->n_var_rec < e->n_surv_rec ? e->n_var_rec : e->n_surv_rec;
+  if (e->d_gphase && e->gphase_n) {  // development aid: k_genc phase split, last generation
+    std::vector<long long> g(e->gphase_n);
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(g.data(), e->d_gphase, g.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    double acc[6] = {0};
+    long long w0 = INT64_MAX, w1 = 0;
+    int n = 0;
+    std::vector<double> dur;
+    for (size_t w = 0; w * 8 < g.size(); ++w) {
+      const long long* q = &g[w * 8];
+      if (!q[0] || !q[5]) continue;
+      for (int k = 1; k <= 5; ++k) acc[k] += (double)(q[k] - q[k - 1]);
+      w0 = std::min(w0, q[6]);
+      w1 = std::max(w1, q[7]);
+      dur.push_back((double)(q[7] - q[6]));
+      ++n;
+    }
+    if (n) {
+      std::sort(dur.begin(), dur.end());
+      std::fprintf(stderr, "[mv] k_genc phase cycles (mean over %d workgroups): stage1=%.0f draws=%.0f "
+                   "rows1=%.0f stage2=%.0f rows2=%.0f | workgroup wall (100 MHz ticks) p50=%.0f "
+                   "max=%.0f, launch span=%lld\n", n, acc[1] / n, acc[2] / n, acc[3] / n,
+                   acc[4] / n, acc[5] / n, dur[dur.size() / 2], dur.back(), w1 - w0);
+    }
+  }
   if (e->d_phase && e->B > 0) {  // development aid: survival phase split of the last generation
     std::vector<long long> ph((size_t)e->B * 32);
     HIPCHK(hipDeviceSynchronize());

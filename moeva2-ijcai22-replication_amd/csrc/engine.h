@@ -133,6 +133,7 @@ struct RowsArgs {
   double sbx_eta;           // SBX distribution index (30)
   int do_eval;              // 0: variation only
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
+  long long* gphase;        // development (MV_GEN_PHASES): k_genc clocks [grid][8], or NULL
 };
 
 // Survival ------------------------------------------------------------------------------

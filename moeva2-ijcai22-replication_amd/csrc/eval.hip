@@ -85,13 +85,15 @@ hipError_t release_rows(int slot, hipStream_t stream) {
 // + 1) << 4, positions and mutated values (crossed parent value through mutate_gene).
 // (A separate one-row-per-lane kernel computing these ahead of k_gen was measured slower:
 // its serial Philox / pow chains sit on the generation's critical path.)
-template <int CAP>
+// `preload` runs once the mating is known, before the mutation draws: the caller issues the
+// first rows' parent loads there, so their latency overlaps the Philox / gather / pow work.
+template <int CAP, class Preload>
 __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, const int b,
                                           const int irow, const bool mine, const int gen,
                                           const bool sbx, const uint32_t* geo, const int* ginfo,
                                           const double* gin, const Rng& rng, int& par_v,
                                           int& cx0_v, int& cx1_v, int& mut_v, int (&mpos)[CAP],
-                                          double (&mval)[CAP]) {
+                                          double (&mval)[CAP], Preload&& preload) {
   const int V = p.V;
   if (mine) {
     const int nm = a.n / 2;
@@ -106,6 +108,7 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
       cx1_v &= 1;
     }
   }
+  preload();
   // (1) mutation positions and their PM uniforms
   const float lq = __log2f(1.0f - 1.0f / (float)V);
 #ifdef MV_DBG_NOMUT
@@ -188,8 +191,8 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
 // SBX: the SBX crossover option compiled in (a separate instance: its pow()-heavy path
 // doubled the two-point kernel's registers, halving its occupancy).
 template <bool IDENT, int NT, bool SBX>
-__device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
-                                         unsigned char* smem) {
+__device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
+                                        unsigned char* smem) {
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -233,6 +236,7 @@ __device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_ro
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 1] = clock64();
   const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
   const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
   const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
@@ -265,15 +269,26 @@ __device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_ro
   const bool mine = lane < nrw;
   const int irow = rc.i0 + wave + VARY_W * lane;
   if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
-  if (a.mode == 1) {
-    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
-                       cx1_v, mut_v, mpos, mval);
-  } else if (mine) {
-    par_v = irow | (irow << 16);
-  }
   auto load_row = [&](int k, double* x) {
     load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x);
   };
+  // Two rows' parent genes in flight ahead of the row being finished: under load an HBM
+  // round trip is ~4 us, several rows' worth of work, and one row of prefetch left each row
+  // waiting on its loads (r03 phase clocks: ~9.6 k cycles per row).  The first two rows'
+  // loads go out before the mutation draws, whose gathers and pow chains then overlap them.
+  double xa[NT], xb[NT];
+  auto preload = [&]() {
+    if (nrw > 0) load_row(0, xa);
+    if (nrw > 1) load_row(1, xb);
+  };
+  if (a.mode == 1) {
+    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
+                       cx1_v, mut_v, mpos, mval, preload);
+  } else {
+    if (mine) par_v = irow | (irow << 16);
+    preload();
+  }
+  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 2] = clock64();
   const bool l2 = p.norm == 2;
   // child genes -> pool, fp32 ML row, f2 (row k of this wave, genes already mutated)
   auto finish_row = [&](int k, const double* x) {
@@ -336,13 +351,14 @@ __device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_ro
       if (a.hist) a.hist[((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w + 1] = f2;
     }
   };
-  double xn[NT];
-  if (nrw > 0) load_row(0, xn);
-  for (int k = 0; k < nrw; ++k) {
+  for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
     double x[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) x[t] = xn[t];
-    if (k + 1 < nrw) load_row(k + 1, xn);
+    for (int t = 0; t < NT; ++t) {
+      x[t] = xa[t];
+      xa[t] = xb[t];
+    }
+    if (k + 2 < nrw) load_row(k + 2, xb);
     if (sbx) {  // SBX children, then every mutation of the row
       const int i = rc.i0 + wave + VARY_W * k;
       const int nm = a.n / 2;
@@ -388,6 +404,7 @@ __device__ __forceinline__ void gen_rows(const RowsArgs& a, int gen, int hist_ro
       finish_row(k, x);
     }
   }
+  return orow_v;  // this lane's row destination (k_genc's phase 2 reuses it)
 }
 
 template <bool IDENT, int NT, bool SBX>
@@ -403,13 +420,39 @@ __global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0
 // evaluates its (register-packed) ops.
 template <bool FULL, bool IDENT, int NT>
 __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int rows_wg,
-                                          unsigned char* smem) {
+                                          unsigned char* smem, bool have_dst = false,
+                                          int dst_pre = 0) {
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
   const int b = rc.b, nrw = rc.nrw;
   const int V = p.V;
   const VaryOff o = vary_offsets(p);
+  // row sources: mode 1 reads the children k_gen wrote (destination rows; k_genc passes the
+  // destinations its phase 1 already loaded), mode 0 the input
+  int src_v = 0, dst_v = 0;
+  if (lane < nrw) {
+    const int i = rc.i0 + wave + CONS_W * lane;
+    dst_v = have_dst ? dst_pre : (a.out_map ? a.out_map[(size_t)b * a.n + i] : i);
+    src_v = a.mode == 1 ? dst_v : i;
+  }
+  const double* gsrc = a.mode == 1 ? a.genes_out + (size_t)b * a.out_rows * V
+                                   : a.genes_in + (size_t)b * a.in_rows * V;
+  // Unconditional (index-clamped) loads: a per-element "if (g < V) load" makes hipcc branch
+  // around each load and wait vmcnt(0) per element, serialising the row's round trips.
+  auto load_row = [&](int k, double* x) {
+    const double* gr = gsrc + (size_t)rdl(src_v, k) * V;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int g = lane + 64 * t;
+      x[t] = gr[g < V ? g : V - 1];
+    }
+  };
+  // two rows in flight (as k_gen); the first two go out before the LDS staging so their
+  // round trips overlap it
+  double xa[NT], xb[NT];
+  if (nrw > 0) load_row(0, xa);
+  if (nrw > 1) load_row(1, xb);
   glds_copy<CONS_T>(smem, p.vblob, o.a_end, wave, lane);
   glds_copy<CONS_T>(smem + o.a_end, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
   int ginf[NT];
@@ -424,6 +467,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
   double* xrow = (double*)(smem + o.a_end + o.x_end + wave * o.rb);
   {
     const double* s_xi = (const double*)(smem + o.a_end + o.xi);
@@ -445,32 +489,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     const int c = lane + 64 * k;
     opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
   }
-  // row sources: mode 1 reads the children k_gen wrote (destination rows), mode 0 the input
-  int src_v = 0, dst_v = 0;
-  if (lane < nrw) {
-    const int i = rc.i0 + wave + CONS_W * lane;
-    dst_v = a.out_map ? a.out_map[(size_t)b * a.n + i] : i;
-    src_v = a.mode == 1 ? dst_v : i;
-  }
-  const double* gsrc = a.mode == 1 ? a.genes_out + (size_t)b * a.out_rows * V
-                                   : a.genes_in + (size_t)b * a.in_rows * V;
-  // Unconditional (index-clamped) loads: a per-element "if (g < V) load" makes hipcc branch
-  // around each load and wait vmcnt(0) per element, serialising the row's round trips.
-  auto load_row = [&](int k, double* x) {
-    const double* gr = gsrc + (size_t)rdl(src_v, k) * V;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int g = lane + 64 * t;
-      x[t] = gr[g < V ? g : V - 1];
-    }
-  };
-  double xn[NT];
-  if (nrw > 0) load_row(0, xn);
-  for (int k = 0; k < nrw; ++k) {
-    double x[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) x[t] = xn[t];
-    if (k + 1 < nrw) load_row(k + 1, xn);
+  auto do_row = [&](int k, const double* x) {
     const int i = rc.i0 + wave + CONS_W * k;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -492,6 +511,16 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
       if (hrow) hrow[2] = f3;
     }
     wave_sync();  // the next row's scatter overwrites xrow
+  };
+  for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
+    double x[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      x[t] = xa[t];
+      xa[t] = xb[t];
+    }
+    if (k + 2 < nrw) load_row(k + 2, xb);
+    do_row(k, x);
   }
 }
 
@@ -512,12 +541,22 @@ __global__ __launch_bounds__(VARY_T) void k_genc(int slot, int gen, int hist_row
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
-  gen_rows<IDENT, NT, SBX>(a, gen, hist_row0, rows_wg, smem);
+  if (a.gphase && threadIdx.x == 0) {
+    a.gphase[(size_t)blockIdx.x * 8 + 0] = clock64();
+    a.gphase[(size_t)blockIdx.x * 8 + 6] = wall_clock64();
+  }
+  const int orow_v = gen_rows<IDENT, NT, SBX>(a, gen, hist_row0, rows_wg, smem);
+  if (a.gphase && threadIdx.x == 0) a.gphase[(size_t)blockIdx.x * 8 + 3] = clock64();
   // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
-  // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them
+  // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them.  Both
+  // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  cons_rows<false, IDENT, NT>(a, hist_row0, rows_wg, smem);
+  cons_rows<false, IDENT, NT>(a, hist_row0, rows_wg, smem, true, orow_v);
+  if (a.gphase && threadIdx.x == 0) {
+    a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
+    a.gphase[(size_t)blockIdx.x * 8 + 7] = wall_clock64();
+  }
 }
 
 // k_narrow: k_gen + k_cons for narrow rows, one lane per row (narrow.h).
