@@ -93,13 +93,14 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
                                           const bool sbx, const uint32_t* geo, const int* ginfo,
                                           const double* gin, const Rng& rng, int& par_v,
                                           int& cx0_v, int& cx1_v, int& mut_v, int (&mpos)[CAP],
-                                          double (&mval)[CAP], Preload&& preload) {
+                                          double (&mval)[CAP], const int2 pre_pr,
+                                          Preload&& preload) {
   const int V = p.V;
   if (mine) {
     const int nm = a.n / 2;
     const int m = irow % nm;
     const int side = irow / nm;
-    const int2 pr = *(const int2*)(a.parents + ((size_t)b * nm + m) * 2);
+    const int2 pr = pre_pr;  // the row's mating, loaded by the caller ahead of its staging
     par_v = side ? (pr.y | (pr.x << 16)) : (pr.x | (pr.y << 16));
     cx0_v = pack_cx(cx_sub(rng, gen, m, 0, p.n_sub[0], a.cx_prob));
     cx1_v = pack_cx(cx_sub(rng, gen, m, 1, p.n_sub[1], a.cx_prob));
@@ -203,6 +204,19 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const VaryOff o = vary_offsets(p);
   const GenLds L = gen_lds(o, REGC, IDENT, ev);
   const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
+  // the rows' matings and destinations first: their round trips (the parents come from the
+  // previous k_survive) overlap the LDS staging instead of following it
+  const bool mine = lane < nrw;
+  const int irow = rc.i0 + wave + VARY_W * lane;
+  int2 pre_pr = make_int2(0, 0);
+  int orow_v = 0;
+  if (mine) {
+    if (a.mode == 1) {
+      const int nm = a.n / 2;
+      pre_pr = *(const int2*)(a.parents + ((size_t)b * nm + irow % nm) * 2);
+    }
+    orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
+  }
   glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
   if (ev && !REGC) {
     glds_copy(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
@@ -253,7 +267,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
 
   // this wave's rows: lane k holds row k's packed parents (own | oth << 16), crossover
   // draws, destination and mutations (count | overflow << 3 | (last position + 1) << 4)
-  int par_v = 0, cx0_v = 0, cx1_v = 0, orow_v = 0, mut_v = 0;
+  int par_v = 0, cx0_v = 0, cx1_v = 0, mut_v = 0;
   int mpos[MUT_CAP];
   double mval[MUT_CAP];
 #pragma unroll
@@ -266,9 +280,6 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
   const double* sgu = a.s.gu + (size_t)b * V;
   const bool sbx = SBX && a.mode == 1;
-  const bool mine = lane < nrw;
-  const int irow = rc.i0 + wave + VARY_W * lane;
-  if (mine) orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
   auto load_row = [&](int k, double* x) {
     load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x);
   };
@@ -283,7 +294,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   };
   if (a.mode == 1) {
     row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
-                       cx1_v, mut_v, mpos, mval, preload);
+                       cx1_v, mut_v, mpos, mval, pre_pr, preload);
   } else {
     if (mine) par_v = irow | (irow << 16);
     preload();
@@ -307,6 +318,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     double acc = 0.0;
     if (IDENT) {  // gene g <-> mutable feature g: no decoding
       const bool wx = !p.xml_direct;  // else k_mlp2 scales the child genes itself
+      float* xd = xo;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int j = lane + 64 * t;
@@ -323,7 +335,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
             const double d = (xf * es + em) - x0;
             acc = l2 ? acc + d * d : nanmax(acc, fabs(d));
           }
-          if (wx) xo[j] = v;
+          if (wx) xd[j] = v;
         }
       }
     } else {  // decode through the row buffer (feature_encoder.py:91-124)
