@@ -370,14 +370,10 @@ def main():
     #   k_gen : parent genes read + child genes written (2*V*8) + fp32 ML row (Dm4*4) + f2 (8)
     #   k_cons: child genes read (V*8) + f3 (8)
     #   k_survive: merged F read (N*3*8) + survivor/free slots + parents (4*(P+O+O)) per state
-    # xml_direct (csrc/engine.h: IDENT problems with a k_mlp2 classifier, the botnet shape):
-    # k_gen writes no fp32 ML row, k_mlp2 reads the child genes itself
+    # xml_direct (mv_get_mlp_kernel = 1: IDENT problems whose classifier is k_mlp2 reading
+    # the genes): k_gen writes no fp32 ML row, k_mlp2 reads the child genes itself
     prog = eng.prog
-    ident = (V == Dm and int((prog.gene_kind == 2).sum()) == 0
-             and np.array_equal(prog.gene_feat, prog.mut_feats))
-    hidden = dims_full[1:-1]
-    xml_direct = (ident and all(h % 16 == 0 and h <= 128 for h in hidden)
-                  and "MV_XML" not in os.environ)
+    xml_direct = kt["mlp_kernel"] == "k_mlp2(genes)"
     gen_bytes = 2 * V * 8 + (0 if xml_direct else Dm4 * 4) + 8
     cons_bytes = V * 8 + 8
     surv_bytes_state = (P + O) * 3 * 8 + 4 * (P + 2 * O)
@@ -413,7 +409,8 @@ def main():
             "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": mlp_peak,
                       "unit": "TFLOP/s", "frac": mlp_tfs / mlp_peak,
                       "traffic": traffic.get("k_mlp"),
-                      "kernel": "k_mlp (%s MFMA Dense chain)" % ("bf16" if bf16 else "fp32"),
+                      "kernel": "%s (%s MFMA Dense chain)" % (kt["mlp_kernel"],
+                                                               "bf16" if bf16 else "fp32"),
                       "achieved_algorithmic": mlp_tfs_alg,
                       "algorithmic_flops_per_launch": eval_flops * rows,
                       "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},

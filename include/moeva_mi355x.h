@@ -235,6 +235,12 @@ int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
  * k_cons events then bracket nothing), 2 = k_genc (k_gen and k_cons as two phases of one
  * launch; likewise).  Lets a profiler attribute ms[0] + ms[1] of mv_get_phase_times. */
 int mv_get_row_kernel(mv_engine* e, int32_t* kind);
+/* The classifier kernel an attack generation runs: 0 = k_mlp (one tile of rows per
+ * workgroup, any widths), 1 = k_mlp2 reading the child genes (no fp32 ML row is written),
+ * 2 = k_mlp2 reading the fp32 ML rows, 3 = k_mlp2x (k_mlp2 with layer 0 fed by an LDS-DMA
+ * ring of the fp32 ML rows), 4 = k_mlpw (bf16 weights), -1 = no device classifier.
+ * Lets a profiler price the ML-row bytes of the row kernel and the classifier. */
+int mv_get_mlp_kernel(mv_engine* e, int32_t* kind);
 
 /* The engine's pow for the variation operators (host build of csrc/detmath.h det_pow, the
  * same IEEE operation sequence as the device code): out[i] = det_pow(x[i], y[i]) for host

@@ -15,6 +15,7 @@
 #include "detmath.h"
 #include "engine.h"
 #include "kernels.h"
+#include "rowops.h"
 
 using namespace mv;
 
@@ -106,6 +107,7 @@ struct mv_engine {
   bool has_model = false;
   long long* d_phase = nullptr;  // MV_SURV_PHASES=1: survival phase clocks [B][16]
   long long* d_gphase = nullptr; // MV_GEN_PHASES=1: k_genc clocks [grid][8] (one group)
+  bool gphase_mlp = false;        // MV_MLP_PHASES=1: the same buffer holds the classifier's
   size_t gphase_n = 0;
   unsigned long long* dom_g = nullptr;  // P + O > SURV_NLDS: survival dominance bitsets
   size_t dom_stride = 0;
@@ -373,7 +375,14 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     // k_mlp2 packing of the hidden layers: Wp[kg][n][16] = W[16 kg + i][n] (zero padded)
     p.mlp2 = 1;
     for (int l = 1; l < md->n_layers; ++l) p.mlp2 &= md->dims[l] % 16 == 0 && md->dims[l] <= 128;
-    p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML");
+    // xml_direct (k_mlp2 builds its layer-0 tiles from the child genes) unless k_mlp2x
+    // runs (MV_MLPX=1, A/B only: that pipeline DMAs the fp32 rows k_genc writes, xml, into
+    // LDS; slower end to end); MV_XML: the xml rows + k_mlp2
+    {
+      const char* mx = std::getenv("MV_MLPX");
+      p.mlpx = mx && mx[0] == '1' && mlpx_ok(p);
+      p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML") && !p.mlpx;
+    }
     for (int l = 0; l + 1 < md->n_layers && p.mlp2; ++l) {
       const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
       const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major
@@ -833,7 +842,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_w = hist_w;
   va.seed = prm->seed;
   va.xml = e->xml;
-  if (std::getenv("MV_GEN_PHASES") && ngrp == 1) {  // development: k_genc phase clocks
+  const bool mlp_ph = std::getenv("MV_MLP_PHASES") != nullptr;
+  if ((std::getenv("MV_GEN_PHASES") || mlp_ph) && ngrp == 1) {  // development: phase clocks
     const size_t n = (size_t)B * O * 8;  // >= grid * 8 (at least one row per workgroup)
     if (e->gphase_n < n) {
       HIPCHK(hipMalloc((void**)&e->d_gphase, n * sizeof(long long)));
@@ -841,7 +851,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
       e->gphase_n = n;
     }
     HIPCHK(hipMemsetAsync(e->d_gphase, 0, n * sizeof(long long), stream));
-    va.gphase = e->d_gphase;
+    (mlp_ph ? va.mphase : va.gphase) = e->d_gphase;
+    e->gphase_mlp = mlp_ph;
   }
   int slot_va[MAX_GROUPS];
   RowsArgs vq[MAX_GROUPS];
@@ -888,6 +899,12 @@ int mv_get_row_kernel(mv_engine* e, int32_t* kind) {
   return MV_OK;
 }
 
+int mv_get_mlp_kernel(mv_engine* e, int32_t* kind) {
+  if (!e || !kind) return fail(MV_ERR_ARG, "null argument");
+  *kind = mlp_kernel_kind(base_rows(e).p);
+  return MV_OK;
+}
+
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations) {
   if (!e) return fail(MV_ERR_ARG, "null engine");
@@ -929,6 +946,13 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
     }
     if (n) {
       std::sort(dur.begin(), dur.end());
+      if (e->gphase_mlp)
+        std::fprintf(stderr, "[mv] k_mlp phase cycles (mean over %d workgroups, first tile): "
+                     "issue=%.0f chunk0=%.0f layer0=%.0f hidden=%.0f final=%.0f | workgroup "
+                     "wall (100 MHz ticks) p50=%.0f max=%.0f, launch span=%lld\n", n, acc[1] / n,
+                     acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, dur[dur.size() / 2],
+                     dur.back(), w1 - w0);
+      else
       std::fprintf(stderr, "[mv] k_genc phase cycles (mean over %d workgroups): stage1=%.0f draws=%.0f "
                    "rows1=%.0f stage2=%.0f rows2=%.0f | workgroup wall (100 MHz ticks) p50=%.0f "
                    "max=%.0f, launch span=%lld\n", n, acc[1] / n, acc[2] / n, acc[3] / n,

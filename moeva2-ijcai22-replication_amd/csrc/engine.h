@@ -94,6 +94,7 @@ struct DProblem {
   // is mutable feature g), so k_gen writes no fp32 ML row: the xml hand-off (Dm4 * 4 B
   // written + read back per row) is gone
   int xml_direct;
+  int mlpx;  // the classifier runs k_mlp2x (MV_MLPX=1 and mlpx_ok; development A/B)
 };
 
 struct DStates {
@@ -134,6 +135,7 @@ struct RowsArgs {
   int do_eval;              // 0: variation only
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
   long long* gphase;        // development (MV_GEN_PHASES): k_genc clocks [grid][8], or NULL
+  long long* mphase;        // development (MV_MLP_PHASES): k_mlp2 / k_mlp2x clocks [grid][8]
 };
 
 // Survival ------------------------------------------------------------------------------

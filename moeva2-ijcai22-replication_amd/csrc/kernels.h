@@ -141,6 +141,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
 // Which kernels launch_gen / launch_cons run for these rows: 0 k_gen + k_cons, 1 k_narrow
 // (launch_cons is empty), 2 k_genc (launch_cons is empty)
 int row_kernel_kind(const RowsArgs& a);
+int mlp_kernel_kind(const DProblem& p);
 hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream);
 hipError_t launch_vary(const RowsArgs& a, int slot, int gen, int hist_row0,
                        hipStream_t stream);

@@ -24,7 +24,8 @@ EXPORTED = [
     "mv_last_error", "mv_device_count", "mv_engine_create", "mv_engine_destroy",
     "mv_set_states", "mv_evaluate", "mv_decode", "mv_constraints", "mv_survive", "mv_select_parents",
     "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
-    "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_get_row_kernel", "mv_set_attack_mode",
+    "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_get_row_kernel",
+    "mv_get_mlp_kernel", "mv_set_attack_mode",
     "mv_set_crossover", "mv_set_mlp_precision",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
@@ -101,6 +102,7 @@ def lib():
             "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
             "mv_get_phase_times": [vp, _f64p, _i32p],
             "mv_get_row_kernel": [vp, _i32p],
+            "mv_get_mlp_kernel": [vp, _i32p],
             "mv_set_attack_mode": [vp, C.c_int32],
             "mv_set_crossover": [vp, C.c_int32, C.c_double, C.c_double],
             "mv_set_mlp_precision": [vp, C.c_int32],
@@ -348,9 +350,13 @@ class Engine:
         check(lib().mv_get_phase_times(self._h, ph, C.byref(n)))
         rk = C.c_int32()
         check(lib().mv_get_row_kernel(self._h, C.byref(rk)))
+        mk = C.c_int32()
+        check(lib().mv_get_mlp_kernel(self._h, C.byref(mk)))
         return {"vary_ms": tv.value, "mlp_ms": tm.value, "survive_ms": ts.value,
                 "gen_ms": ph[0], "cons_ms": ph[1], "generations": n.value,
-                "row_kernel": ("k_gen+k_cons", "k_narrow", "k_genc")[rk.value]}
+                "row_kernel": ("k_gen+k_cons", "k_narrow", "k_genc")[rk.value],
+                "mlp_kernel": {-1: None, 0: "k_mlp", 1: "k_mlp2(genes)", 2: "k_mlp2",
+                               3: "k_mlp2x", 4: "k_mlpw"}[mk.value]}
 
 
 def survive(F, ref_points, n_survive, mu, seed, gen, ideal, worst, extreme, has_extreme,

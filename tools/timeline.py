@@ -13,7 +13,7 @@ import sys
 from collections import defaultdict
 
 KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_genc": "k_genc<", "k_narrow": "k_narrow<",
-        "k_mlp": "k_mlp2<", "k_predict": "k_predict<", "k_survive": "k_survive<"}
+        "k_mlp": "k_mlp2<", "k_mlp2x": "k_mlp2x<", "k_predict": "k_predict<", "k_survive": "k_survive<"}
 
 
 def key(name):
