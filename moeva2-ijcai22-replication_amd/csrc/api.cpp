@@ -844,7 +844,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.xml = e->xml;
   const bool mlp_ph = std::getenv("MV_MLP_PHASES") != nullptr;
   if ((std::getenv("MV_GEN_PHASES") || mlp_ph) && ngrp == 1) {  // development: phase clocks
-    const size_t n = (size_t)B * O * 8;  // >= grid * 8 (at least one row per workgroup)
+    const size_t n = (size_t)B * O * 16;  // >= grid * 16 (at least one row per workgroup)
     if (e->gphase_n < n) {
       HIPCHK(hipMalloc((void**)&e->d_gphase, n * sizeof(long long)));
       e->attack_allocs.push_back(e->d_gphase);
@@ -935,8 +935,12 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
     long long w0 = INT64_MAX, w1 = 0;
     int n = 0;
     std::vector<double> dur;
-    for (size_t w = 0; w * 8 < g.size(); ++w) {
-      const long long* q = &g[w * 8];
+    const size_t stride = e->gphase_mlp ? 16 : 8;
+    double sub[4] = {0};
+    for (size_t w = 0; w * stride + stride <= g.size(); ++w) {
+      const long long* q = &g[w * stride];
+      if (stride == 16 && q[8] && q[12])
+        for (int k = 0; k < 4; ++k) sub[k] += (double)(q[9 + k] - q[8 + k]);
       if (!q[0] || !q[5]) continue;
       for (int k = 1; k <= 5; ++k) acc[k] += (double)(q[k] - q[k - 1]);
       w0 = std::min(w0, q[6]);
@@ -949,9 +953,10 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
       if (e->gphase_mlp)
         std::fprintf(stderr, "[mv] k_mlp phase cycles (mean over %d workgroups, first tile): "
                      "issue=%.0f chunk0=%.0f layer0=%.0f hidden=%.0f final=%.0f | workgroup "
-                     "wall (100 MHz ticks) p50=%.0f max=%.0f, launch span=%lld\n", n, acc[1] / n,
+                     "wall (100 MHz ticks) p50=%.0f max=%.0f, launch span=%lld | chunk 2: "
+                     "loads=%.0f mfma=%.0f store=%.0f barrier=%.0f\n", n, acc[1] / n,
                      acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, dur[dur.size() / 2],
-                     dur.back(), w1 - w0);
+                     dur.back(), w1 - w0, sub[0] / n, sub[1] / n, sub[2] / n, sub[3] / n);
       else
       std::fprintf(stderr, "[mv] k_genc phase cycles (mean over %d workgroups): stage1=%.0f draws=%.0f "
                    "rows1=%.0f stage2=%.0f rows2=%.0f | workgroup wall (100 MHz ticks) p50=%.0f "

@@ -827,8 +827,8 @@ __global__ __launch_bounds__(EVAL_T) void k_mlp(int slot, int hist_row0) {
 // k_gen through a double-buffered LDS chunk of 64 k (register staged); hidden outputs go to
 // an LDS ping-pong; the immutable features' contribution to layer 0 is the per-state bias
 // bias1 (k_setup_states).  The last Dense + softmax is a dot product per row on the VALU.
-template <int CJ, bool BF, bool DIRECT>
-__global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int hist_row0) {
+template <int CJ, bool BF, bool DIRECT, bool CO>
+__global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 2 : 1)) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
@@ -867,12 +867,13 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     double gd[DIRECT ? 4 : 1][4];
     // xml_direct: the source rows are the tile's child genes (fp64) in the pool, ML-scaled
     // here exactly as k_gen would have, (float)(x * mlS + mlM); row u of this thread:
-    // tile row (tid >> 4) + 16 u
-    const double* grow[4];
+    // tile row (tid >> 4) + 16 u (CO: (tid >> 5) + 8 u, see the fp32 loop)
+    constexpr int NGR = CO ? 8 : 4;
+    const double* grow[NGR];
     if (DIRECT) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int rr0 = r0 + (tid >> 4) + 16 * u;
+      for (int u = 0; u < NGR; ++u) {
+        const int rr0 = r0 + (CO ? (tid >> 5) + 8 * u : (tid >> 4) + 16 * u);
         const int rr = rr0 < a.total ? rr0 : a.total - 1;
         const int st = rr / a.n, i = rr - st * a.n;
         grow[u] = a.mode == 1
@@ -929,35 +930,204 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
     }                                                                                    \
   }
     const bool ph = a.mphase && tid == 0 && tile == (int)blockIdx.x;
-    long long* phq = a.mphase + (size_t)blockIdx.x * 8;
+    long long* phq = a.mphase + (size_t)blockIdx.x * 16;
     if (ph) {
       phq[0] = clock64();
       phq[6] = wall_clock64();
     }
-    M2_CHUNK_LOAD(0)
-    if (ph) phq[1] = clock64();
-    __syncthreads();  // the previous tile's readers of rowst / A0 / H are done
-    if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
-    M2_CHUNK_STORE(0, 0)
-    __syncthreads();
-    if (ph) phq[2] = clock64();
     floatx4 acc[CJ][4];
 #pragma unroll
     for (int cj = 0; cj < CJ; ++cj)
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < nch; ++c) {
-      if (c + 1 < nch) M2_CHUNK_LOAD(c + 1)
-      const int ng = min(4, nkg0 - 4 * c);
-      if (BF)
-        mlp2_layer_bf<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, 16 * ng, p.Wb[0], 2 * c, N0,
-                          acc, tile_map(N0 >> 4, wave), il, ka);
-      else
-        mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
-                       p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, tile_map(N0 >> 4, wave),
-                       il, ka);
-      if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1, c + 1)
+    float b1[CJ][4][4];    // fp32 path: bias1 of the layer-0 outputs this lane writes
+    int fin_mc = 0, fin_orow = 0;  // fp32 path, tid < 64: min_class and output row of row tid
+    if constexpr (BF) {
+      M2_CHUNK_LOAD(0)
+      if (ph) phq[1] = clock64();
+      __syncthreads();  // the previous tile's readers of rowst / A0 / H are done
+      if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
+      M2_CHUNK_STORE(0, 0)
       __syncthreads();
+      if (ph) phq[2] = clock64();
+      for (int c = 0; c < nch; ++c) {
+        if (c + 1 < nch) M2_CHUNK_LOAD(c + 1)
+        const int ng = min(4, nkg0 - 4 * c);
+        if (BF)
+          mlp2_layer_bf<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD, 16 * ng, p.Wb[0], 2 * c, N0,
+                            acc, tile_map(N0 >> 4, wave), il, ka);
+        else
+          mlp2_layer<CJ>(A0 + (c & 1) * M2_ROWS * M2_ALD, M2_ALD,
+                         p.Wp[0] + (size_t)4 * c * N0 * 16, ng, N0, acc, tile_map(N0 >> 4, wave),
+                         il, ka);
+        if (c + 1 < nch) M2_CHUNK_STORE((c + 1) & 1, c + 1)
+        __syncthreads();
+      }
+    } else {
+      // fp32 layer 0, software-pipelined with one register set per operand.  Iteration c
+      // issues the source rows of chunk c + 1, runs chunk c's MFMAs on W(c) -- loaded at the
+      // end of iteration c - 1, so OLDER than those rows, and since vmcnt retires in order
+      // the MFMAs' wait leaves the rows in flight (the previous version loaded each k-group's
+      // weights after the rows, so its first MFMA waited out the rows' HBM round trip: ~10 k
+      // cycles per 2 k-cycle chunk, MV_MLP_PHASES) -- then loads W(c + 1), converts chunk
+      // c + 1 into the other LDS buffer (waiting for its rows; only W(c + 1) is younger) and
+      // ends on an LDS-only barrier.  Loads use clamped indices, never a condition (a
+      // conditional load makes hipcc wait vmcnt(0) where the paths join).
+      const TileMap m0 = tile_map(N0 >> 4, wave);
+      const int nct0 = N0 >> 4;
+      const float* Wp0 = p.Wp[0];
+      const int q = tid & 15;  // this thread's 4-k piece of every staged row
+      float4 wr[4][CJ];
+      double gd[DIRECT ? 4 : 1][4];
+      float4 st[DIRECT ? 1 : 4];
+      // CO (genes per row even, so rows start 16-B aligned): lane-contiguous staging --
+      // thread (row (tid >> 5) + 8 u, piece p = tid & 31) loads the 16 B of genes
+      // 2p, 2p + 1 of the chunk, so a wave's load covers two rows' 512 B without gaps
+      // (the 4-genes-per-thread mapping touched every 128-B line with four dwordx2 loads)
+      const int pc = tid & 31;
+      uint4 gv[CO ? 8 : 1];
+#define M2F_LOADW(c)                                                                      \
+  {                                                                                       \
+    _Pragma("unroll") for (int g = 0; g < 4; ++g) {                                       \
+      const int kg = 4 * (c) + g < nkg0 ? 4 * (c) + g : nkg0 - 1;                         \
+      _Pragma("unroll") for (int cj = 0; cj < CJ; ++cj) {                                 \
+        const int ct = m0.cb + 4 * cj < nct0 ? m0.cb + 4 * cj : nct0 - 1;                 \
+        wr[g][cj] = *(const float4*)(Wp0 + ((size_t)kg * N0 + ct * 16 + il) * 16 + 4 * ka); \
+      }                                                                                   \
+    }                                                                                     \
+  }
+#define M2F_LOADG(c)                                                                      \
+  if constexpr (CO) {                                                                     \
+    const int cc = (c) < nch ? (c) : nch - 1;                                             \
+    const int k = cc * 64 + 2 * pc + 1 < K0dm ? cc * 64 + 2 * pc : K0dm - 2;              \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u)                                         \
+      gv[CO ? u : 0] = *(const uint4*)(grow[u] + k);                                      \
+  } else {                                                                                \
+    const int cc = (c) < nch ? (c) : nch - 1;                                             \
+    const int k = cc * 64 + 4 * q < K0 ? cc * 64 + 4 * q : K0 - 4;                        \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                       \
+      if (DIRECT) {                                                                       \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                   \
+          const int kk = k + e < K0dm ? k + e : K0dm - 1;                                 \
+          gd[DIRECT ? u : 0][e] = grow[u][kk];                                            \
+        }                                                                                 \
+      } else {                                                                            \
+        const int row = (tid >> 4) + 16 * u;                                              \
+        const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                       \
+        st[DIRECT ? 0 : u] = *(const float4*)(a.xml + (size_t)rr * K0 + k);              \
+      }                                                                                   \
+    }                                                                                     \
+  }
+#define M2F_STORE(c)                                                                      \
+  if constexpr (CO) {                                                                     \
+    const int k = (c) * 64 + 2 * pc;                                                      \
+    float* Ab = A0 + ((c) & 1) * M2_ROWS * M2_ALD;                                        \
+    const int k0 = k < K0 ? k : K0 - 1, k1 = k + 1 < K0 ? k + 1 : K0 - 1;                 \
+    const double sc0 = sS[k0], sc1 = sS[k1], mn0 = sM[k0], mn1 = sM[k1];                  \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                       \
+      const int row = (tid >> 5) + 8 * u;                                                 \
+      const uint4 w = gv[CO ? u : 0];                                                     \
+      const double d0 = __hiloint2double((int)w.y, (int)w.x);                             \
+      const double d1 = __hiloint2double((int)w.w, (int)w.z);                             \
+      float2 v;                                                                           \
+      v.x = k < K0dm ? (float)(d0 * sc0 + mn0) : 0.f;                                     \
+      v.y = k + 1 < K0dm ? (float)(d1 * sc1 + mn1) : 0.f;                                 \
+      *(float2*)(Ab + row * M2_ALD + 2 * pc) = v;                                         \
+    }                                                                                     \
+  } else {                                                                                \
+    const int kq = (c) * 64 + 4 * q;                                                      \
+    const int k = kq < K0 ? kq : K0 - 4;                                                  \
+    float* Ab = A0 + ((c) & 1) * M2_ROWS * M2_ALD;                                        \
+    double sc[4], mn[4];                                                                  \
+    if (DIRECT) {                                                                         \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                     \
+        sc[e] = sS[k + e];                                                                \
+        mn[e] = sM[k + e];                                                                \
+      }                                                                                   \
+    }                                                                                     \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                       \
+      const int row = (tid >> 4) + 16 * u;                                                \
+      float4 v;                                                                           \
+      if (DIRECT) {                                                                       \
+        float v4[4];                                                                      \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e)                                     \
+          v4[e] = k + e < K0dm ? (float)(gd[DIRECT ? u : 0][e] * sc[e] + mn[e]) : 0.f;    \
+        v = make_float4(v4[0], v4[1], v4[2], v4[3]);                                      \
+      } else {                                                                            \
+        v = st[DIRECT ? 0 : u];                                                           \
+      }                                                                                   \
+      *(float4*)(Ab + row * M2_ALD + 4 * q) = v;                                          \
+    }                                                                                     \
+  }
+#define M2F_MARK(c, k) \
+  if (ph && (c) == 2) phq[k] = clock64();
+      M2F_LOADG(0)
+      M2F_LOADW(0)
+      if (ph) phq[1] = clock64();
+      // the previous tile's readers of rowst / A0 / H are done (LDS only: no vmcnt(0))
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
+      M2F_STORE(0)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // the layer-0 epilogue's per-state bias (bias1) and the final phase's per-row scalars,
+      // loaded now (unconditionally) so that their latency hides under the chunk loop
+#pragma unroll
+      for (int cj = 0; cj < CJ; ++cj) {
+        const int ct = m0.cb + 4 * cj < nct0 ? m0.cb + 4 * cj : nct0 - 1;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int row = (m0.rt0 + (rt < m0.nrt ? rt : 0)) * 16 + ka * 4 + jj;
+            const int st0 = rowst[row];
+            b1[cj][rt][jj] = a.s.bias1[(size_t)(st0 < 0 ? 0 : st0) * N0 + ct * 16 + il];
+          }
+      }
+      {
+        const int rr = r0 + (tid & 63) < a.total ? r0 + (tid & 63) : a.total - 1;
+        const int stc = rr / a.n;
+        fin_mc = a.s.min_class[stc];
+        // out_map may be NULL (mode 0): read a valid dummy instead of branching
+        const int* om = a.out_map ? a.out_map : a.s.min_class;
+        const int ov = om[a.out_map ? rr : stc];
+        fin_orow = a.out_map ? ov : rr - stc * a.n;
+      }
+      if (ph) phq[2] = clock64();
+      for (int c = 0; c < nch; ++c) {
+        M2F_MARK(c, 8)
+        M2F_LOADG(c + 1)
+        M2F_MARK(c, 9)
+        {
+          const int ng = min(4, nkg0 - 4 * c);
+          const float* Ab = A0 + (c & 1) * M2_ROWS * M2_ALD;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g < ng) {
+              float4 af[4];
+#pragma unroll
+              for (int rt = 0; rt < 4; ++rt) {
+                const int r = m0.rt0 + (rt < m0.nrt ? rt : 0);
+                af[rt] = *(const float4*)(Ab + (r * 16 + il) * M2_ALD + g * 16 + 4 * ka);
+              }
+              mfma_k4<CJ>(af, wr[g], acc, m0.cb, nct0, m0.nrt);
+            }
+          }
+        }
+        M2F_MARK(c, 10)
+        M2F_LOADW(c + 1)
+        if (c + 1 < nch) M2F_STORE(c + 1)
+        M2F_MARK(c, 11)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        M2F_MARK(c, 12)
+      }
+#undef M2F_LOADW
+#undef M2F_LOADG
+#undef M2F_STORE
+#undef M2F_MARK
+      __syncthreads();  // the trailing (clamped, unused) prefetches land before H reuses A0
     }
 #undef M2_CHUNK_LOAD
 #undef M2_CHUNK_STORE
@@ -992,8 +1162,12 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
               const int row = (m.rt0 + rt) * 16 + ka * 4 + j;
               float bv;
               if (l == 0) {
-                const int s = rowst[row];
-                bv = a.s.bias1[(size_t)(s < 0 ? 0 : s) * N0 + col];
+                if constexpr (BF) {
+                  const int s = rowst[row];
+                  bv = a.s.bias1[(size_t)(s < 0 ? 0 : s) * N0 + col];
+                } else {
+                  bv = b1[cj][rt][j];
+                }
               } else {
                 bv = p.bias[l][col];
               }
@@ -1049,10 +1223,10 @@ __global__ __launch_bounds__(256, CJ == 1 ? 3 : 2) void k_mlp2(int slot, int his
             mx = z[c] > mx ? z[c] : mx;
           }
         }
-        const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
+        const double f1 = softmax_pick(z, nout, mx, BF ? a.s.min_class[s] : fin_mc);
         const int i = r0 + tid - s * a.n;
         if (a.F) {
-          const int orow = a.out_map ? a.out_map[(size_t)s * a.n + i] : i;
+          const int orow = BF ? (a.out_map ? a.out_map[(size_t)s * a.n + i] : i) : fin_orow;
           a.F[((size_t)s * a.out_rows + orow) * 3] = f1;
         }
         if (a.hist) a.hist[((size_t)s * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
@@ -1143,7 +1317,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp2x(int slot, int hist_row0) {
     }                                                                                     \
   }
     const bool ph = a.mphase && tid == 0 && tile == (int)blockIdx.x;
-    long long* phq = a.mphase + (size_t)blockIdx.x * 8;
+    long long* phq = a.mphase + (size_t)blockIdx.x * 16;
     if (ph) {
       phq[0] = clock64();
       phq[6] = wall_clock64();
@@ -1187,19 +1361,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp2x(int slot, int hist_row0) {
           const int R = (m.rt0 + (rt < m.nrt ? rt : 0)) * 16 + il;
           af[rt] = *(const float4*)(As + R * 64 + (((4 * g + ka) ^ il) << 2));
         }
-#pragma unroll
-        for (int cj = 0; cj < CJ; ++cj) {
-          if (m.cb + 4 * cj < nct0) {
-#pragma unroll
-            for (int rt = 0; rt < 4; ++rt) {
-              if (rt >= m.nrt) continue;
-              acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].x, bf[cj].x, acc[cj][rt], 0, 0, 0);
-              acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].y, bf[cj].y, acc[cj][rt], 0, 0, 0);
-              acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].z, bf[cj].z, acc[cj][rt], 0, 0, 0);
-              acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].w, bf[cj].w, acc[cj][rt], 0, 0, 0);
-            }
-          }
-        }
+        mfma_k4<CJ>(af, bf, acc, m.cb, nct0, m.nrt);
       }
       // every wave is done reading the slot before it is refilled
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1940,19 +2102,19 @@ static int cu_count() {
   return n;
 }
 
-template <int CJ, bool BF, bool DIRECT>
+template <int CJ, bool BF, bool DIRECT, bool CO>
 static hipError_t mlp2_go3(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static bool configured = false;
   static size_t occ_lds = 0;
   static int occ = 2;
   if (!configured) {
-    allow_lds(k_mlp2<CJ, BF, DIRECT>);
+    allow_lds(k_mlp2<CJ, BF, DIRECT, CO>);
     configured = true;
   }
   const size_t lds = mlp2_lds(a.p);
   if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF, DIRECT>, 256, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF, DIRECT, CO>, 256, lds) != hipSuccess ||
         n < 1)
       n = 1;
     (void)hipGetLastError();
@@ -1961,15 +2123,20 @@ static hipError_t mlp2_go3(const RowsArgs& a, int slot, int hist_row0, hipStream
   }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
   const int grid = ntiles < occ * cu_count() ? ntiles : occ * cu_count();
-  hipLaunchKernelGGL((k_mlp2<CJ, BF, DIRECT>), dim3(grid), dim3(256), lds, stream, slot,
+  hipLaunchKernelGGL((k_mlp2<CJ, BF, DIRECT, CO>), dim3(grid), dim3(256), lds, stream, slot,
                      hist_row0);
   return hipGetLastError();
 }
 
 template <int CJ, bool BF>
 static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
-  return a.p.xml_direct ? mlp2_go3<CJ, BF, true>(a, slot, hist_row0, stream)
-                        : mlp2_go3<CJ, BF, false>(a, slot, hist_row0, stream);
+  // CO: the fp32 path's lane-contiguous gene staging (rows of an even gene count start
+  // 16-B aligned in the pool); MV_MLP_CO=0 turns it off (A/B)
+  static const bool co_env = !(std::getenv("MV_MLP_CO") && std::getenv("MV_MLP_CO")[0] == '0');
+  if (a.p.xml_direct && !BF && co_env && (a.p.Dm & 1) == 0)
+    return mlp2_go3<CJ, BF, true, true>(a, slot, hist_row0, stream);
+  return a.p.xml_direct ? mlp2_go3<CJ, BF, true, false>(a, slot, hist_row0, stream)
+                        : mlp2_go3<CJ, BF, false, false>(a, slot, hist_row0, stream);
 }
 
 template <int CJ>

@@ -572,6 +572,42 @@ __device__ __forceinline__ TileMap tile_map(int nct, int wave) {
   return TileMap{wave % cw, (wave / cw) * cw, cw};
 }
 
+// One k-group's 16 fp32 MFMAs per (column tile cj, row tile rt) accumulator: k-step s
+// (the float4 component) is the OUTER loop, so consecutive MFMAs write different
+// accumulators and never wait for each other's result (a dependent v_mfma_f32_16x16x4f32
+// waits out its predecessor's full latency: the rt-outer order ran the layer-0 chunk at ~3x
+// its MFMA issue time).  Every accumulator still sums its k in the order x, y, z, w, so
+// the result is bit-identical to the rt-outer order.
+__device__ __forceinline__ float f4c(const float4& v, int s) {
+  return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+}
+template <int CJ>
+__device__ __forceinline__ void mfma_k4(const float4 (&af)[4], const float4 (&bf)[CJ],
+                                        floatx4 (&acc)[CJ][4], int cb, int nct, int nrt) {
+  if (nrt == 4) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int cj = 0; cj < CJ; ++cj)
+        if (cb + 4 * cj < nct)
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+            acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(af[rt], s), f4c(bf[cj], s),
+                                                               acc[cj][rt], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int cj = 0; cj < CJ; ++cj)
+        if (cb + 4 * cj < nct)
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+            if (rt < nrt)
+              acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(af[rt], s), f4c(bf[cj], s),
+                                                                 acc[cj][rt], 0, 0, 0);
+  }
+}
+
 template <int CJ>
 __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
                                            const float* __restrict__ Wp, int nkg, int N,
@@ -603,19 +639,7 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
     float4 bn[CJ], an[4];
     load_b(kg + 1, bn);  // next group's weights (L2) while this group's MFMAs run
     load_a(kg + 1, an);
-#pragma unroll
-    for (int cj = 0; cj < CJ; ++cj) {
-      if (wave + 4 * cj < nct) {
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          if (rt >= m.nrt) continue;
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].x, bf[cj].x, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].y, bf[cj].y, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].z, bf[cj].z, acc[cj][rt], 0, 0, 0);
-          acc[cj][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rt].w, bf[cj].w, acc[cj][rt], 0, 0, 0);
-        }
-      }
-    }
+    mfma_k4<CJ>(af, bf, acc, wave, nct, m.nrt);
 #pragma unroll
     for (int cj = 0; cj < CJ; ++cj) bf[cj] = bn[cj];
 #pragma unroll
