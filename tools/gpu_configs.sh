@@ -15,3 +15,5 @@ run c3_lcld_augmented 300 --workload rq4.lcld.moeva_augmented --steps 2 --warmup
 run c2_botnet_bf16 300 --workload rq1.botnet.static --mlp-dtype bf16 --steps 2 --warmup 1 --no-cpu-baseline
 MV_MLPW=1 run c2_botnet_bf16_mlpw 300 --workload rq1.botnet.static --mlp-dtype bf16 --steps 2 --warmup 1 --no-cpu-baseline
 run c4_lcld_scaleout 600 --workload synthetic.lcld.scaleout --steps 1 --warmup 1 --no-cpu-baseline
+run c2_botnet_sbx 300 --workload rq1.botnet.static --crossover sbx --steps 2 --warmup 1 --no-cpu-baseline
+run c5_botnet_wide_bf16 600 --workload synthetic.botnet.wide --mlp-dtype bf16 --steps 1 --warmup 1 --no-cpu-baseline
