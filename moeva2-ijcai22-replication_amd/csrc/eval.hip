@@ -375,8 +375,10 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       const int i = rc.i0 + wave + VARY_W * k;
       const int nm = a.n / 2;
       const int pr = rdl(par_v, k);
-      sbx_row<NT>(x, ginf, gin + (size_t)(pr >> 16) * V, sgl, sgu, V, i % nm, i / nm,
-                  rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen, a.sbx_eta, lane);
+      unsigned char* sb = smem + gen_sbx_at(L) + (size_t)wave * gen_sbx_wave_bytes(NT);
+      sbx_row<NT>(x, ginf, gin + (size_t)(pr & 0xFFFF) * V, gin + (size_t)(pr >> 16) * V, sgl,
+                  sgu, V, i % nm, i / nm, rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen,
+                  a.sbx_eta, lane, (int*)(sb + 64 * NT * 8), (double*)sb);
       mutate_row_full<NT>(x, s_geo, s_ginfo, sgl, sgu, V, i, rng, gen, a.eta, lane);
     } else if (a.mode == 1) {  // apply the row's cached mutations
       apply_row_mutations<NT>(x, rdl(mut_v, k) & 7, mpos, mval, k, lane);
@@ -2016,10 +2018,11 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const dim3 grid(B * ((a.n + rw - 1) / rw));
     const int nt = genc_nt(a.p);
     const VaryOff o = vary_offsets(a.p);
-    const size_t lg = gen_lds(o, gen_regc(a.p, nt), true, true).total;
+    const bool sbx = a.mode == 1 && a.cx_kind == 1;
+    const GenLds gl = gen_lds(o, gen_regc(a.p, nt), true, true);
+    const size_t lg = sbx ? gen_lds_sbx(gl, nt) : gl.total;
     const size_t lc = cons_lds_total(o);
     const size_t lds = lg > lc ? lg : lc;
-    const bool sbx = a.mode == 1 && a.cx_kind == 1;
     if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
     if (nt == 5) return genc_go<5>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
     if (nt == 6) return genc_go<6>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
@@ -2032,8 +2035,9 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
   const dim3 grid(B * ((a.n + rw - 1) / rw));
   const int nt = vary_nt(a.p);
   const bool ident = a.p.ident != 0;
-  const size_t lds = gen_lds(vary_offsets(a.p), gen_regc(a.p, nt), ident, a.do_eval != 0).total;
   const bool sbx = a.mode == 1 && a.cx_kind == 1;
+  const GenLds gl = gen_lds(vary_offsets(a.p), gen_regc(a.p, nt), ident, a.do_eval != 0);
+  const size_t lds = sbx ? gen_lds_sbx(gl, nt) : gl.total;
 #define GEN(I, N) return gen_go<I, N>(grid, lds, stream, slot, gen, hist_row0, rw, sbx)
   if (ident) {
     if (nt == 1) GEN(true, 1);

@@ -110,6 +110,13 @@ __host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool iden
   l.total = at;
   return l;
 }
+// SBX rows: a per-wave list of the crossed genes (int) and their children (double) after the
+// k_gen layout (rowops.h sbx_row)
+__host__ __device__ inline unsigned gen_sbx_at(const GenLds& l) { return (l.total + 15u) & ~15u; }
+__host__ __device__ inline unsigned gen_sbx_wave_bytes(int nt) { return 64u * (unsigned)nt * 12u; }
+__host__ __device__ inline unsigned gen_lds_sbx(const GenLds& l, int nt) {
+  return gen_sbx_at(l) + VARY_W * gen_sbx_wave_bytes(nt);
+}
 // k_cons LDS: region A, region X, one row per wave
 __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + CONS_W * o.rb;

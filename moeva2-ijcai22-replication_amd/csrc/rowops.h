@@ -346,31 +346,63 @@ constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream 
 // Philox word (index m * MUT_J + g, TAG_SBX): bit 0 = 0 -> the variable crosses
 // (prob_per_variable 0.5), bit 1 -> swap c1/c2, words y, z -> calc_betaq's uniform.  The
 // mating-level draw (prob 0.9) of each subset comes from TAG_CX as for two-point.
+// The crossed genes' children are computed spread over the wave's lanes: pass 1 finds the
+// genes that cross (each lane its genes lane + 64 t) and appends their indices to the wave's
+// LDS list sdesc in (t, lane) order; pass 2 gives item s of the list to lane s % 64 in round
+// s / 64, which recomputes the gene's draw and inputs and writes the child to sres[s]; pass
+// 3 hands each child back.  With the children computed in place (one t at a time) every lane
+// paid for all NT slots' two det_pow chains whenever any lane of the slot crossed; spread,
+// a row costs ceil(crossed / 64) rounds.  Same draws, same arithmetic: bit-identical.
 template <int NT>
-__device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double* goth,
-                                        const double* gl, const double* gu, int V, int m,
-                                        int side, int on0, int on1, const Rng& rng, int gen,
-                                        double eta, int lane) {
+__device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double* gown,
+                                        const double* goth, const double* gl, const double* gu,
+                                        int V, int m, int side, int on0, int on1, const Rng& rng,
+                                        int gen, double eta, int lane, int* sdesc,
+                                        double* sres) {
+  int slot[NT];
+  int cnt = 0;  // wave-uniform
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int g = lane + 64 * t;
-    if (g >= V) continue;
-    const bool real = (ginf[t] & 3) == 0;
-    if (!(real ? on0 : on1)) continue;
-    const double own = x[t], oth = goth[g];
-    const double p0 = side == 0 ? own : oth, p1 = side == 0 ? oth : own;
-    const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
-    if ((w.x & 1u) || !(fabs(p0 - p1) > 1.0e-14)) continue;
-    const double lo = gl[g], hi = gu[g];
-    double c = sbx_child(p0, p1, real ? lo : lo - INT_WIDEN, real ? hi : hi + INT_WIDEN,
-                         u53(w.y, w.z), (w.x & 2u) != 0u, side, eta);
-    if (!real) {
-      c = rint(c);
-      if (c < lo) c = lo;
-      if (c > hi) c = hi;
+    bool need = false;
+    if (g < V) {
+      const bool real = (ginf[t] & 3) == 0;
+      if (real ? on0 : on1) {
+        const double own = x[t], oth = goth[g];
+        const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
+        need = !(w.x & 1u) && fabs(own - oth) > 1.0e-14;
+      }
     }
-    x[t] = c;
+    const unsigned long long mask = __ballot(need);
+    const int s = cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    slot[t] = need ? s : -1;
+    if (need) sdesc[s] = g | (((ginf[t] & 3) == 0 ? 1 : 0) << 16);
+    cnt += __popcll(mask);
   }
+  for (int r = 0; r < cnt; r += 64) {
+    const int s = r + lane;
+    if (s < cnt) {
+      const int d = sdesc[s];
+      const int g = d & 0xFFFF;
+      const bool real = (d >> 16) != 0;
+      const double own = gown[g], oth = goth[g];
+      const double p0 = side == 0 ? own : oth, p1 = side == 0 ? oth : own;
+      const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
+      const double lo = gl[g], hi = gu[g];
+      double c = sbx_child(p0, p1, real ? lo : lo - INT_WIDEN, real ? hi : hi + INT_WIDEN,
+                           u53(w.y, w.z), (w.x & 2u) != 0u, side, eta);
+      if (!real) {
+        c = rint(c);
+        if (c < lo) c = lo;
+        if (c > hi) c = hi;
+      }
+      sres[s] = c;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    if (slot[t] >= 0) x[t] = sres[slot[t]];
 }
 
 // Every mutation of row i (the whole geometric-gap draw sequence of mutation_draws, no
