@@ -1119,7 +1119,9 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
         }
         M2F_MARK(c, 10)
         M2F_LOADW(c + 1)
-        if (c + 1 < nch) M2F_STORE(c + 1)
+        if (c + 1 < nch) {
+          M2F_STORE(c + 1)
+        }
         M2F_MARK(c, 11)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
