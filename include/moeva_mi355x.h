@@ -209,6 +209,15 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
 /* 0: auto (default), 1: per-phase kernel chain -- the same schedule.  2 (the retired
  * whole-attack kernel, measured slower than the chain) is rejected with MV_ERR_ARG. */
 int mv_set_attack_mode(mv_engine* e, int32_t mode);
+/* Random streams of the bound states (no reference counterpart; an engine option).
+ * enabled = 0 (default, the reference's behaviour): every state draws from the same Philox
+ * stream, as Moeva2 re-seeds each state's pymoo.minimize with the same seed
+ * (moeva2.py:158-165).  enabled = 1: state b draws from its own stream, keyed by its GLOBAL
+ * index first_state + b (pass the shard's offset under sharding, so results do not depend on
+ * the GPU count).  Each state's attack is statistically the same either way; across states
+ * the outcomes become independent, which is what the end-to-end parity test needs to resolve
+ * 1 pp (tests/test_gpu_e2e.py).  Applies to mv_attack_run and mv_variation. */
+int mv_set_state_streams(mv_engine* e, int32_t enabled, int64_t first_state);
 /* Classifier precision of the engine's fitness path (mv_evaluate, mv_attack_run): 0 = fp32
  * (default; the parity mode: exact fp32 products on v_mfma_f32_16x16x4f32, as Keras computes
  * classifier.py:23-29), 1 = bf16 perf mode (hidden-layer weights and activations rounded to
@@ -241,6 +250,19 @@ int mv_get_row_kernel(mv_engine* e, int32_t* kind);
  * ring of the fp32 ML rows), 4 = k_mlpw (bf16 weights), -1 = no device classifier.
  * Lets a profiler price the ML-row bytes of the row kernel and the classifier. */
 int mv_get_mlp_kernel(mv_engine* e, int32_t* kind);
+
+/* Device index checks (debug builds compiled with -DMV_CHECKS, `make checks`): synchronises
+ * the device, then returns and clears the first failed check of the row, classifier and
+ * survival kernels since the last call -- record[0] check code (csrc/check.h; 0 = none),
+ * [1] workgroup, [2] thread, [3] value, [4] bound, [5] number of failures -- and *compiled = 1
+ * in a checks build (0 otherwise: record is all zero).  A checks build also fails
+ * mv_attack_population with MV_ERR_STATE when a check failed.  No reference counterpart. */
+int mv_debug_checks(int32_t* record, int32_t* compiled);
+/* Checks builds: the inputs of the first survival whose survivors were not distinct (check
+ * 26) -- out[3096] doubles: [0] 1 if valid, [1] generation, [2] state in its group, [3] N,
+ * [4..6] carried ideal, [7..9] worst, [10..18] extremes, [19] has_extreme, [20] n_survive,
+ * [21] seed (uint64 bits), [24..24+3N) merged F.  Cleared by the call; zeros otherwise. */
+int mv_debug_survival_dump(double* out);
 
 /* The engine's pow for the variation operators (host build of csrc/detmath.h det_pow, the
  * same IEEE operation sequence as the device code): out[i] = det_pow(x[i], y[i]) for host

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/moeva_mi355x.h"
+#include "check.h"
 #include "detmath.h"
 #include "engine.h"
 #include "kernels.h"
@@ -140,6 +141,8 @@ struct mv_engine {
   // profiling
   int cx_kind = 0;          // 0: two-point (reference), 1: SBX
   double sbx_eta = 30.0, cx_prob = 0.9;
+  int state_keys = 0;       // mv_set_state_streams: state b draws from stream key0 + b
+  uint32_t key0 = 0;
   int attack_mode = 0;      // 0: auto, 1: per-phase chain (the only schedule)
   bool profiling = false;
   std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
@@ -485,6 +488,8 @@ static RowsArgs base_rows(const mv_engine* e) {
   a.cx_prob = e->cx_prob;
   a.cx_kind = e->cx_kind;
   a.sbx_eta = e->sbx_eta;
+  a.state_keys = e->state_keys;
+  a.key0 = e->key0;
   a.mut_thr = (uint32_t)(4294967296.0 / (double)e->p.V);
   a.do_eval = 1;
   a.p.mlp_bf16 = e->has_model && e->mlp_bf16;
@@ -740,6 +745,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     r.s.bias1 += b0 * H1;
     r.s.min_class += b0;
     r.total = r.s.B * n_per_state;
+    r.key0 += (uint32_t)b0;  // per-state streams: the group's first state
     if (r.genes_in) r.genes_in += b0 * r.in_rows * V;
     if (r.genes_out) r.genes_out += b0 * r.out_rows * V;
     if (r.parents) r.parents += b0 * O;
@@ -762,6 +768,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     s.worst += b0 * 3;
     s.extreme += b0 * 9;
     s.has_extreme += b0;
+    s.key0 += (uint32_t)b0;
     if (s.parents_out) s.parents_out += b0 * O;
     if (s.phase) s.phase += b0 * 32;
     if (s.dom_g) s.dom_g += b0 * s.dom_stride;
@@ -792,6 +799,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.R = R;
   sa.mu = prm->mu;
   sa.seed = prm->seed;
+  sa.state_keys = e->state_keys;
+  sa.key0 = e->key0;
   sa.ideal = e->ideal;
   sa.worst = e->worst;
   sa.extreme = e->extreme;
@@ -1016,6 +1025,14 @@ int mv_set_crossover(mv_engine* e, int32_t kind, double eta, double prob) {
   e->cx_kind = kind;
   e->sbx_eta = eta;
   e->cx_prob = prob;
+  return MV_OK;
+}
+
+int mv_set_state_streams(mv_engine* e, int32_t enabled, int64_t first_state) {
+  if (!e || enabled < 0 || enabled > 1 || first_state < 0 || first_state > 0x7FFFFFFF)
+    return fail(MV_ERR_ARG, "state streams: enabled 0 or 1, 0 <= first_state < 2^31");
+  e->state_keys = enabled;
+  e->key0 = (uint32_t)first_state;
   return MV_OK;
 }
 
@@ -1305,11 +1322,41 @@ int mv_objcalc_score(mv_objcalc* o, int32_t B, int32_t n, const double* x_init, 
   return MV_OK;
 }
 
+int mv_debug_checks(int32_t* record, int32_t* compiled) {
+  if (!record) return fail(MV_ERR_ARG, "null record");
+  if (compiled) *compiled = MV_CHECKS_ON;
+  HIPCHK(hipDeviceSynchronize());
+  int ev[8], sv[8];
+  HIPCHK(take_checks_eval(ev));
+  HIPCHK(take_checks_survive(sv));
+  const int* r = ev[0] ? ev : sv;
+  for (int k = 0; k < 8; ++k) record[k] = r[k];
+  record[5] = ev[5] + sv[5];
+  return MV_OK;
+}
+
+int mv_debug_survival_dump(double* out) {
+  if (!out) return fail(MV_ERR_ARG, "null dump buffer");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(take_survival_dump(out));
+  return MV_OK;
+}
+
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
   if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(launch_gather_pop(e->B, e->P, e->p.V, e->S, e->pop_slot, e->pool, e->poolF, genes, F,
                            (hipStream_t)stream));
+  if (MV_CHECKS_ON) {  // checks build: a failed device index check fails the attack loudly
+    int32_t r[8];
+    if (mv_debug_checks(r, nullptr) != MV_OK) return MV_ERR_HIP;
+    if (r[0])
+      return fail(MV_ERR_STATE, "device index check " + std::to_string(r[0]) + " failed (block " +
+                                    std::to_string(r[1]) + ", thread " + std::to_string(r[2]) +
+                                    ", value " + std::to_string(r[3]) + ", bound " +
+                                    std::to_string(r[4]) + ", " + std::to_string(r[5]) +
+                                    " failures)");
+  }
   return MV_OK;
 }
 

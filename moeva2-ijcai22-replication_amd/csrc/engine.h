@@ -127,6 +127,8 @@ struct RowsArgs {
   int hist_rows, hist_w;
   uint64_t seed;
   uint32_t stream_key;
+  int state_keys;           // 1: state b draws from stream stream_key + key0 + b (per-state
+  uint32_t key0;            //    streams, mv_set_state_streams); 0: every state shares stream_key
   uint32_t mut_thr;         // floor(2^32 / V)
   double eta;               // 20
   double cx_prob;           // 0.9
@@ -155,6 +157,8 @@ struct SurvArgs {
   uint64_t seed;
   int gen;
   uint32_t stream_key;
+  int state_keys;           // as RowsArgs
+  uint32_t key0;
   double* ideal;            // [B][3]
   double* worst;            // [B][3]
   double* extreme;          // [B][9]

@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <mutex>
 
+#include "check.h"
 #include "engine.h"
 #include "kernels.h"
 #include "narrow.h"
@@ -165,10 +166,12 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   }
   const int cntk = __shfl(cnt, kk), park = __shfl(par_v, kk);
   const int c0k = __shfl(cx0_v, kk), c1k = __shfl(cx1_v, kk);
-  const int mp = pq < 0 ? 0 : pq;  // unconditional, clamped loads
+  const int mp = MV_IDX(pq < 0 ? 0 : pq, V, CK_GEN_MUTPOS);  // unconditional, clamped loads
   const int gi = ginfo[mp];
-  double xv = gin[(size_t)(swapped_packed(gi, c0k, c1k) ? (park >> 16) : (park & 0xFFFF)) * V + mp];
-  const double lo = gl[mp], hi = gu[mp];
+  const int mrow = MV_IDX(swapped_packed(gi, c0k, c1k) ? (park >> 16) : (park & 0xFFFF),
+                          a.in_rows, CK_GEN_MUTROW);
+  double xv = gin[MV_IDX((size_t)mrow * V + mp, (long long)a.in_rows * V, CK_AT_MUTLOAD)];
+  const double lo = gl[MV_IDX(mp, V, CK_AT_BOUNDS)], hi = gu[MV_IDX(mp, V, CK_AT_BOUNDS)];
   if (qq < cntk) xv = mutate_gene(xv, lo, hi, (gi & 3) == 0, uq, a.eta);
 #pragma unroll
   for (int q = 0; q < CAP; ++q) mval[q] = __shfl(xv, (lane * 4 + q) & 63);  // back to row lanes
@@ -198,7 +201,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk(a.n, rows_wg, wave);
-  const int b = rc.b, nrw = rc.nrw;
+  const int b = MV_IDX(rc.b, a.total / a.n, CK_GEN_STATE), nrw = rc.nrw;
   const int V = p.V, Dm = p.Dm, Dm4 = p.Dm4;
   const bool ev = a.do_eval != 0;
   const VaryOff o = vary_offsets(p);
@@ -214,8 +217,10 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (a.mode == 1) {
       const int nm = a.n / 2;
       pre_pr = *(const int2*)(a.parents + ((size_t)b * nm + irow % nm) * 2);
+      pre_pr.x = MV_IDX(pre_pr.x, a.in_rows, CK_GEN_PARENT);
+      pre_pr.y = MV_IDX(pre_pr.y, a.in_rows, CK_GEN_PARENT);
     }
-    orow_v = a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow;
+    orow_v = MV_IDX(a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow, a.out_rows, CK_GEN_DST);
   }
   glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
   if (ev && !REGC) {
@@ -276,12 +281,14 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     mval[q] = 0.0;
   }
   const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
-  const Rng rng(a.seed, a.stream_key);
+  const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
   const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
   const double* sgu = a.s.gu + (size_t)b * V;
   const bool sbx = SBX && a.mode == 1;
   auto load_row = [&](int k, double* x) {
-    load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x);
+    k = MV_IDX(k, min(nrw, 64), CK_GEN_LANE);
+    load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x,
+                        (long long)a.in_rows * V);
   };
   // Two rows' parent genes in flight ahead of the row being finished: under load an HBM
   // round trip is ~4 us, several rows' worth of work, and one row of prefetch left each row
@@ -305,13 +312,15 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   auto finish_row = [&](int k, const double* x) {
     int Vo = V, Dmo = Dm, Dm4o = Dm4;
     asm volatile("" : "+s"(Vo), "+s"(Dmo), "+s"(Dm4o));
-    const int i = rc.i0 + wave + VARY_W * k;
-    const int orow = rdl(orow_v, k);
+    const int i = MV_IDX(rc.i0 + wave + VARY_W * k, a.n, CK_GEN_ROW);
+    const int orow = rdl(orow_v, MV_IDX(k, min(nrw, 64), CK_GEN_LANE));
     if (a.genes_out) {
-      double* gout = a.genes_out + ((size_t)b * a.out_rows + orow) * V;
+      double* gout = a.genes_out + (size_t)b * a.out_rows * V;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (lane + 64 * t < Vo) gout[lane + 64 * t] = x[t];
+        if (lane + 64 * t < Vo)
+          gout[MV_IDX((size_t)orow * V + lane + 64 * t, (long long)a.out_rows * V, CK_AT_CHILD)] =
+              x[t];
     }
     if (!ev) return;
     float* xo = a.xml + ((size_t)b * a.n + i) * Dm4;
@@ -359,8 +368,12 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (lane == 0) {
       double f2 = l2 ? sqrt(acc) : acc;
       if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-      if (a.F) a.F[((size_t)b * a.out_rows + orow) * 3 + 1] = f2;
-      if (a.hist) a.hist[((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w + 1] = f2;
+      if (a.F)
+        a.F[(size_t)b * a.out_rows * 3 + MV_IDX((size_t)orow * 3 + 1, a.out_rows * 3, CK_AT_F2)] = f2;
+      if (a.hist)
+        a.hist[(size_t)b * a.hist_rows * a.hist_w +
+               MV_IDX((size_t)MV_IDX(hist_row0 + i, a.hist_rows, CK_GEN_ROW) * a.hist_w + 1,
+                      (long long)a.hist_rows * a.hist_w, CK_AT_HIST1)] = f2;
     }
   };
   for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
@@ -390,7 +403,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   if (a.mode == 1 && __ballot(mut_v & 8)) {
     const RowsArgs* ap = &a;
     const uint64_t seed2 = *(volatile const uint64_t*)&ap->seed;
-    const Rng rng2(seed2, a.stream_key);
+    const Rng rng2(seed2, state_stream(a.stream_key, a.state_keys, a.key0, b));
     const double* gl = a.s.gl + (size_t)b * V;
     const double* gu = a.s.gu + (size_t)b * V;
     const float lq = __log2f(1.0f - 1.0f / (float)V);
@@ -409,7 +422,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
         for (int t = 0; t < NT; ++t)
           if (pos == lane + 64 * t) xv = x[t];
         if ((pos & 63) == lane) {
-          xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
+          xv = mutate_gene(xv, gl[MV_IDX(pos, V, CK_AT_BOUNDS)], gu[MV_IDX(pos, V, CK_AT_BOUNDS)],
+                         (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
 #pragma unroll
           for (int t = 0; t < NT; ++t)
             if (pos == lane + 64 * t) x[t] = xv;
@@ -439,7 +453,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
-  const int b = rc.b, nrw = rc.nrw;
+  const int b = MV_IDX(rc.b, a.total / a.n, CK_GEN_STATE), nrw = rc.nrw;
   const int V = p.V;
   const VaryOff o = vary_offsets(p);
   // row sources: mode 1 reads the children k_gen wrote (destination rows; k_genc passes the
@@ -447,19 +461,21 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   int src_v = 0, dst_v = 0;
   if (lane < nrw) {
     const int i = rc.i0 + wave + CONS_W * lane;
-    dst_v = have_dst ? dst_pre : (a.out_map ? a.out_map[(size_t)b * a.n + i] : i);
-    src_v = a.mode == 1 ? dst_v : i;
+    dst_v = MV_IDX(have_dst ? dst_pre : (a.out_map ? a.out_map[(size_t)b * a.n + i] : i),
+                   a.out_rows, CK_CONS_DST);
+    src_v = MV_IDX(a.mode == 1 ? dst_v : i, a.mode == 1 ? a.out_rows : a.in_rows, CK_CONS_DST);
   }
   const double* gsrc = a.mode == 1 ? a.genes_out + (size_t)b * a.out_rows * V
                                    : a.genes_in + (size_t)b * a.in_rows * V;
   // Unconditional (index-clamped) loads: a per-element "if (g < V) load" makes hipcc branch
   // around each load and wait vmcnt(0) per element, serialising the row's round trips.
   auto load_row = [&](int k, double* x) {
-    const double* gr = gsrc + (size_t)rdl(src_v, k) * V;
+    const size_t r0 = (size_t)rdl(src_v, MV_IDX(k, min(nrw, 64), CK_GEN_LANE)) * V;
+    const long long lim = (long long)(a.mode == 1 ? a.out_rows : a.in_rows) * V;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int g = lane + 64 * t;
-      x[t] = gr[g < V ? g : V - 1];
+      x[t] = gsrc[MV_IDX(r0 + (g < V ? g : V - 1), lim, CK_AT_SRC2)];
     }
   };
   // two rows in flight (as k_gen); the first two go out before the LDS staging so their
@@ -496,6 +512,10 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   tab.C = p.C;
   tab.n_lane = p.C - p.n_sumdiff;
   tab.tol = p.tol;
+  if (a.hist) {
+    tab.hlo = a.hist + (size_t)b * a.hist_rows * a.hist_w;
+    tab.hhi = tab.hlo + (size_t)a.hist_rows * a.hist_w;
+  }
   unsigned opw[OPS_REG];
   const int kops = min(OPS_REG, (tab.n_lane + 63) >> 6);
 #pragma unroll
@@ -504,7 +524,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
   }
   auto do_row = [&](int k, const double* x) {
-    const int i = rc.i0 + wave + CONS_W * k;
+    const int i = MV_IDX(rc.i0 + wave + CONS_W * k, a.n, CK_CONS_DST);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (lane + 64 * t < V) {
@@ -516,13 +536,23 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     }
     wave_sync();
     double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-    double* hrow =
-        a.hist ? a.hist + ((size_t)b * a.hist_rows + hist_row0 + i) * a.hist_w : nullptr;
+    double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows +
+                                      MV_IDX(hist_row0 + i, a.hist_rows, CK_CONS_DST)) * a.hist_w
+                          : nullptr;
     const double f3 = constraints_regs<FULL>(tab, opw, kops, xrow, lane, grow,
                                              (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
+    // The row's destination is read from lane k HERE, with every lane active: a readlane
+    // of a lane that is inactive at that point returns an undefined value.  (Round 3 read
+    // it inside the lane-0 branch below.  Whenever the compiler spilled dst_v, its reload
+    // ran under that branch's one-lane EXEC mask, so lane k held a stale register value and
+    // f3 was stored at a wild address.  That was the illegal-address fault of the
+    // __launch_bounds__(VARY_T, 4) build, caught by the checks build as CK_AT_F3.)
+    const int dst = rdl(dst_v, k);
     if (lane == 0) {
-      if (a.F) a.F[((size_t)b * a.out_rows + rdl(dst_v, k)) * 3 + 2] = f3;
-      if (hrow) hrow[2] = f3;
+      if (a.F)
+        a.F[(size_t)b * a.out_rows * 3 + MV_IDX((size_t)dst * 3 + 2, a.out_rows * 3, CK_AT_F3)] =
+            f3;
+      if (hrow) *MV_PTR(hrow + 2, tab.hlo, tab.hhi, CK_AT_HIST2) = f3;
     }
     wave_sync();  // the next row's scatter overwrites xrow
   };
@@ -550,8 +580,15 @@ __global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int ro
 // the chain loses a launch boundary; the phases run one after the other, so the kernel
 // needs the larger of the two register and LDS footprints, not their sum (the fused row
 // loop of round 2, k_rows, kept both phases' registers live: 208 VGPRs).
+// MV_GENC_WAVES (development builds): k_genc's minimum waves per SIMD for the register
+// allocator (4: 128 VGPRs; the default, none, lets it use 148 and runs 3 per SIMD)
+#ifdef MV_GENC_WAVES
+#define MV_GENC_BOUNDS __launch_bounds__(VARY_T, MV_GENC_WAVES)
+#else
+#define MV_GENC_BOUNDS __launch_bounds__(VARY_T)
+#endif
 template <bool IDENT, int NT, bool SBX>
-__global__ __launch_bounds__(VARY_T) void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
+__global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -879,8 +916,9 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
         const int rr = rr0 < a.total ? rr0 : a.total - 1;
         const int st = rr / a.n, i = rr - st * a.n;
         grow[u] = a.mode == 1
-            ? a.genes_out + ((size_t)st * a.out_rows + (a.out_map ? a.out_map[rr] : i)) * K0dm
-            : a.genes_in + ((size_t)st * a.in_rows + i) * K0dm;
+            ? a.genes_out + ((size_t)st * a.out_rows +
+                             MV_IDX(a.out_map ? a.out_map[rr] : i, a.out_rows, CK_MLP_ROW)) * K0dm
+            : a.genes_in + ((size_t)st * a.in_rows + MV_IDX(i, a.in_rows, CK_MLP_ROW)) * K0dm;
       }
     }
 #define M2_CHUNK_LOAD(c)                                                                 \
@@ -1094,7 +1132,7 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
         // out_map may be NULL (mode 0): read a valid dummy instead of branching
         const int* om = a.out_map ? a.out_map : a.s.min_class;
         const int ov = om[a.out_map ? rr : stc];
-        fin_orow = a.out_map ? ov : rr - stc * a.n;
+        fin_orow = MV_IDX(a.out_map ? ov : rr - stc * a.n, a.out_rows, CK_MLP_OUT);
       }
       if (ph) phq[2] = clock64();
       for (int c = 0; c < nch; ++c) {
@@ -1230,10 +1268,14 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
         const double f1 = softmax_pick(z, nout, mx, BF ? a.s.min_class[s] : fin_mc);
         const int i = r0 + tid - s * a.n;
         if (a.F) {
-          const int orow = BF ? (a.out_map ? a.out_map[(size_t)s * a.n + i] : i) : fin_orow;
-          a.F[((size_t)s * a.out_rows + orow) * 3] = f1;
+          const int orow = BF ? MV_IDX(a.out_map ? a.out_map[(size_t)s * a.n + i] : i, a.out_rows,
+                                       CK_MLP_OUT)
+                              : fin_orow;
+          a.F[((size_t)MV_IDX(s, a.total / a.n, CK_MLP_OUT) * a.out_rows + orow) * 3] = f1;
         }
-        if (a.hist) a.hist[((size_t)s * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
+        if (a.hist)
+          a.hist[((size_t)s * a.hist_rows + MV_IDX(hist_row0 + i, a.hist_rows, CK_MLP_OUT)) *
+                 a.hist_w] = f1;
       }
     }
     if (ph) {
@@ -2295,6 +2337,8 @@ hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double*
     hipLaunchKernelGGL(k_constraints<false>, grid, dim3(256), lds, stream, slot, n, x, G);
   return hipGetLastError();
 }
+
+MV_DEFINE_TAKE_CHECKS(take_checks_eval)
 
 hipError_t launch_setup_states(int slot, int B, const double* x_init, const double* xl,
                                const double* xu, const float* W1full, const float* b1, double* gl,

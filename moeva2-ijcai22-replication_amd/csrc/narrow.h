@@ -141,7 +141,7 @@ __device__ __forceinline__ void narrow_rows(const RowsArgs& a, int gen, int hist
   const double* gt = go;                   // other parent
   CxSub c0{0, 0, 0}, c1{0, 0, 0};
   int m = 0;
-  const Rng rng(a.seed, a.stream_key);
+  const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
   if (a.mode == 1) {  // two-point crossover of the mating's subsets (k_gen load_row)
     const int nm = a.n / 2;
     m = i % nm;

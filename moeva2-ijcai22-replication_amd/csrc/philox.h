@@ -58,6 +58,14 @@ struct Rng {
   }
 };
 
+// The Philox stream of state b: shared by every state (the reference re-seeds each state's
+// pymoo.minimize with the same seed, moeva2.py:158-165) or, with per-state streams
+// (mv_set_state_streams), one stream per global state id key0 + b.
+__device__ __forceinline__ uint32_t state_stream(uint32_t sk, int state_keys, uint32_t key0,
+                                                 int b) {
+  return state_keys ? sk + key0 + (uint32_t)b : sk;
+}
+
 // 53-bit uniform in [0,1): MT19937 genrand_res53 form on two Philox words.
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);

@@ -1,6 +1,7 @@
 // Device building blocks of the row kernels (variation, constraint program, Dense chain),
 // shared by the per-phase kernels (eval.hip) and the whole-attack kernel (attack.hip).
 #pragma once
+#include "check.h"
 #include "detmath.h"
 #include "engine.h"
 #include "kernels.h"
@@ -36,6 +37,8 @@ struct OpTab {
   const int* pool;      // [n_pool]
   int C, n_lane;        // ops [0, n_lane) lane-parallel, [n_lane, C) ABS_SUMDIFF
   double tol;
+  const double* hlo = nullptr;  // checks builds: the state's history / G range [hlo, hhi)
+  const double* hhi = nullptr;
 };
 
 __device__ __forceinline__ OpTab global_tab(const DProblem& p) {
@@ -186,8 +189,9 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
         v = eval_op<FULL>(t, c, xrow);
       if (v <= t.tol) v = 0.0;
       const double g = v * (v > 0.0 ? 1.0 : 0.0);
-      if (grow) grow[t.col[c]] = g;
-      if (hcols) hcols[t.col[c]] = g;
+      const int col = MV_IDX(t.col[c], t.C, CK_CONS_COL);
+      if (grow) grow[col] = g;
+      if (hcols) *MV_PTR(hcols + col, t.hlo, t.hhi, CK_AT_HIST2) = g;
       acc3 += g;
     }
   }
@@ -196,7 +200,7 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
     if (v <= t.tol) v = 0.0;
     const double g = v * (v > 0.0 ? 1.0 : 0.0);
     if (grow) grow[t.col[c]] = g;
-    if (hcols) hcols[t.col[c]] = g;
+    if (hcols) *MV_PTR(hcols + MV_IDX(t.col[c], t.C, CK_CONS_COL), t.hlo, t.hhi, CK_AT_HIST2) = g;
     acc3 += g;
   }
   double sdsum = 0.0;  // ABS_SUMDIFF columns (wave-uniform values)
@@ -206,7 +210,8 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
     const double g = v * (v > 0.0 ? 1.0 : 0.0);
     if (lane == 0) {
       if (grow) grow[t.col[c]] = g;
-      if (hcols) hcols[t.col[c]] = g;
+      if (hcols)
+        *MV_PTR(hcols + MV_IDX(t.col[c], t.C, CK_CONS_COL), t.hlo, t.hhi, CK_AT_HIST2) = g;
     }
     sdsum += g;
   }
@@ -384,7 +389,7 @@ __device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double
     const int s = r + lane;
     if (s < cnt) {
       const int d = sdesc[s];
-      const int g = d & 0xFFFF;
+      const int g = MV_IDX(d & 0xFFFF, V, CK_GEN_SBX);
       const bool real = (d >> 16) != 0;
       const double own = gown[g], oth = goth[g];
       const double p0 = side == 0 ? own : oth, p1 = side == 0 ? oth : own;
@@ -688,7 +693,7 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
 template <int NT>
 __device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, int V, int pr,
                                                 int cx0, int cx1, const int (&ginf)[NT],
-                                                int lane, double* x) {
+                                                int lane, double* x, long long pool_elems = 0) {
   int Vo = V;
   asm volatile("" : "+s"(Vo));  // keep the per-t bounds out of loop-invariant hoisting
   const unsigned own = (unsigned)(pr & 0xFFFF) * (unsigned)Vo;
@@ -702,7 +707,7 @@ __device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, 
     const unsigned gc = (unsigned)(g < Vo ? g : Vo - 1);
     const bool real = (ginf[t] & 3) == 0;
     const unsigned d = (unsigned)(((ginf[t] >> 2) & 0x7FFF) - (real ? lo0 : lo1));
-    x[t] = gin[(d < (real ? n0 : n1) ? oth : own) + gc];
+    x[t] = gin[MV_IDX((d < (real ? n0 : n1) ? oth : own) + gc, pool_elems, CK_AT_PARENT)];
   }
 }
 
@@ -715,7 +720,7 @@ __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, const i
 #pragma unroll
   for (int q = 0; q < CAP; ++q) {
     if (q < nmut) {
-      const int pos = rdl(mpos[q], k);
+      const int pos = MV_IDX(rdl(mpos[q], k), 64 * NT, CK_GEN_APPLY);
       const double y = rdl_d(mval[q], k);
       const int tt = pos >> 6;
       const bool me = lane == (pos & 63);

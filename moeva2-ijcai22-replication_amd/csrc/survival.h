@@ -18,7 +18,14 @@
 #pragma once
 #include <limits.h>
 
+#include "check.h"
 #include "engine.h"
+#ifdef MV_CHECKS
+namespace mv {
+static __device__ int g_surv_dump_owner;
+static __device__ double g_surv_dump[SURV_DUMP_N];
+}  // namespace mv
+#endif
 #include "philox.h"
 #include "wave.h"
 
@@ -272,7 +279,7 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
     const int a = perm[2 * t], b = perm[2 * t + 1];
     const unsigned bit = rng.draw((uint32_t)t, (uint32_t)gen, TAG_SEL_CHOICE).x & 1u;
     const int w = bit ? b : a;
-    out[t] = map_slot ? map_slot[w] : w;
+    out[t] = map_slot ? map_slot[MV_IDX(w, P, CK_SURV_PARENT)] : w;
   }
 }
 
@@ -347,6 +354,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     const double* src;
     if (slot_mode) {
       s = m < a.P ? a.pop_slot[(size_t)b * a.P + m] : a.free_slot[(size_t)b * a.O + (m - a.P)];
+      s = MV_IDX(s, a.S, CK_SURV_SLOT);
       src = a.F + ((size_t)b * a.S + s) * 3;
     } else {
       src = a.F + ((size_t)b * N + m) * 3;
@@ -934,7 +942,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     const int Lc = n_ranked - fs;
     const int n_rem = nf == 1 ? a.n_survive : a.n_survive - fs;
     const int until = nf == 1 ? 0 : fs;
-    const Rng rng(a.seed, a.stream_key);
+    const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
     int* grank = L.memb;
     int* lev = L.csr;
     int* cnt = L.count;
@@ -1092,13 +1100,42 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   __syncthreads();
   if (slot_mode && N > a.n_survive) {
     const int nfree = block_compact<T>(N, [&](int m) { return L.memb[m] == 0; }, L.key, 0, wsum);
+#ifdef MV_CHECKS
+    if (nfree != N - n_out) {  // duplicate survivors: record, dump this state's inputs
+      if (tid == 0) chk_fail(CK_SURV_DUP, (long long)gen * 4096 + b, nfree);
+      __shared__ int s_own;
+      if (tid == 0) s_own = atomicCAS(&g_surv_dump_owner, 0, 1) == 0;
+      __syncthreads();
+      if (s_own) {
+        double* d = g_surv_dump;
+        for (int m = tid; m < N; m += T)
+          for (int k = 0; k < 3; ++k)
+            d[SURV_DUMP_HEAD + m * 3 + k] = a.F[((size_t)b * a.S + L.slot[m]) * 3 + k];
+        if (tid < 3) {
+          d[4 + tid] = pre_ideal;
+          d[7 + tid] = pre_worst;
+        }
+        if (tid < 9) d[10 + tid] = pext[tid];
+        if (tid == 0) {
+          d[1] = gen;
+          d[2] = b;
+          d[3] = N;
+          d[19] = has_ext;
+          d[20] = a.n_survive;
+          d[21] = __longlong_as_double((long long)a.seed);
+          d[0] = 1.0;
+        }
+      }
+    }
+#endif
     for (int k = tid; k < nfree; k += T)
-      a.free_slot[(size_t)b * a.O + k] = L.slot[L.key[k]];
+      a.free_slot[(size_t)b * a.O + MV_IDX(k, a.O, CK_SURV_SLOT)] = L.slot[L.key[k]];
   }
   __syncthreads();
   PHASE(8)
   if (parents_out) {
-    tournament<T>(a.n_survive, a.O_next, a.seed, a.stream_key, sel_gen, slot_mode ? L.sel : nullptr,
+    tournament<T>(a.n_survive, a.O_next, a.seed,
+                  state_stream(a.stream_key, a.state_keys, a.key0, b), sel_gen, slot_mode ? L.sel : nullptr,
                parents_out + (size_t)b * n_m_next * 2, L.sortk, L.perm);
   }
   __syncthreads();

@@ -2,6 +2,7 @@
 // k_survive wraps survival.h's survive_state; k_select, k_init_pool, k_gather_pop.
 #include <limits.h>
 
+#include "check.h"
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
@@ -58,6 +59,23 @@ __global__ void k_gather_pop(int B, int P, int V, int S, const int* pop_slot, co
       for (int g = threadIdx.x; g < V; g += blockDim.x) genes[t * V + g] = pool[(b * S + s) * V + g];
     if (F && threadIdx.x < 3) F[t * 3 + threadIdx.x] = poolF[(b * S + s) * 3 + threadIdx.x];
   }
+}
+
+MV_DEFINE_TAKE_CHECKS(take_checks_survive)
+
+hipError_t take_survival_dump(double* out) {
+#ifdef MV_CHECKS
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_surv_dump), SURV_DUMP_N * sizeof(double));
+  if (e != hipSuccess) return e;
+  const int z = 0;
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_surv_dump_owner), &z, sizeof(int));
+  if (e != hipSuccess) return e;
+  static double zero[SURV_DUMP_N];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_surv_dump), zero, SURV_DUMP_N * sizeof(double));
+#else
+  for (int k = 0; k < SURV_DUMP_N; ++k) out[k] = 0.0;
+  return hipSuccess;
+#endif
 }
 
 size_t surv_lds_bytes(int N, int R, int Pperm) { return surv_offsets(N, R, Pperm).total; }

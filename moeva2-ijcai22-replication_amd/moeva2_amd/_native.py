@@ -29,7 +29,8 @@ EXPORTED = [
     "mv_set_crossover", "mv_set_mlp_precision",
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
-    "mv_objcalc_score", "mv_det_pow",
+    "mv_objcalc_score", "mv_det_pow", "mv_debug_checks", "mv_set_state_streams",
+    "mv_debug_survival_dump",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -114,6 +115,9 @@ def lib():
             "mv_objcalc_score": [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_int32, vp, C.c_int32,
                                  C.c_int32, vp, vp, vp],
             "mv_det_pow": [C.c_int64, _f64p, _f64p, _f64p],
+            "mv_debug_checks": [_i32p, _i32p],
+            "mv_set_state_streams": [vp, C.c_int32, C.c_int64],
+            "mv_debug_survival_dump": [_f64p],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -132,6 +136,23 @@ def lib():
 def check(rc: int):
     if rc != 0:
         raise NativeError(f"libmoeva_mi355x error {rc}: {lib().mv_last_error().decode()}")
+
+
+def debug_checks():
+    """(compiled, record) of the device index checks (csrc/check.h; a -DMV_CHECKS build):
+    record = [code, workgroup, thread, value, bound, failures], cleared by the call.
+    Synchronises the device."""
+    rec = (C.c_int32 * 8)()
+    on = C.c_int32(0)
+    check(lib().mv_debug_checks(rec, C.byref(on)))
+    return bool(on.value), list(rec)[:6]
+
+
+def debug_survival_dump() -> np.ndarray:
+    """Checks builds: the first duplicate-survivor state's inputs (mv_debug_survival_dump)."""
+    out = np.zeros(24 + 3 * 1024)
+    check(lib().mv_debug_survival_dump(out.ctypes.data_as(_f64p)))
+    return out
 
 
 def det_pow(x, y) -> np.ndarray:
@@ -322,6 +343,12 @@ class Engine:
         """"two_point" (the reference's operator) or "sbx" (SimulatedBinaryCrossover)."""
         check(lib().mv_set_crossover(self._h, {"two_point": 0, "sbx": 1}[kind], float(eta),
                                      float(prob)))
+
+    def set_state_streams(self, enabled: bool, first_state: int = 0):
+        """Per-state random streams (engine option, off = the reference's shared draws):
+        state b draws from Philox stream first_state + b, its GLOBAL index."""
+        check(lib().mv_set_state_streams(self._h, 1 if enabled else 0, int(first_state)))
+        self.state_streams = (bool(enabled), int(first_state))
 
     def set_mlp_precision(self, dtype: str = "fp32"):
         """Classifier precision of the fitness path: "fp32" (parity default) or "bf16" (perf

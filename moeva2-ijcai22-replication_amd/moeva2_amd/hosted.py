@@ -74,6 +74,9 @@ def hosted_attack(eng, plugins: HostPlugins, genes0, minimize_class, n_gen, P, O
     genes (B, P, V), F (B, P, 3) and the history (B, P + (n_gen-1) O, 3 | 3 + C) or None."""
     import torch
 
+    if getattr(eng, "state_streams", (False, 0))[0]:
+        raise ValueError("per-state random streams are a device-loop option (mv_attack_run); "
+                         "the host-plugin loop draws every state from the shared stream")
     dev = torch.device("cuda", eng.device)
     B, V = genes0.shape
     g0 = torch.as_tensor(np.ascontiguousarray(genes0, np.float64), device=dev)

@@ -15,6 +15,7 @@ commits per-seed, per-state o1..o7 as ``tests/golden/e2e_<config>_seeds.npz``.
 
     python tests/golden/make_e2e_seeds.py botnet_rq1 [n_seeds]   # 387 states x 1000 gens
     python tests/golden/make_e2e_seeds.py lcld_rq1_g100 [n_seeds]
+    python tests/golden/make_e2e_seeds.py botnet_rq1_ps [n_seeds]  # per-state streams
 
 Seeds are ``SEED0 + k`` (oracle) -- disjoint from the device test's seeds, so the two
 samples are independent.  The file is rewritten after every completed seed and a rerun
@@ -37,6 +38,14 @@ CONFIGS = {
     "lcld_rq1_g100": ("lcld", 64, 100, 200, 100, 0.2, 0.25),
     "lcld_rq1_g1000": ("lcld", 64, 1000, 200, 100, 0.2, 0.25),
 }
+# "<name>_ps": the same attack with PER-STATE random streams -- state b draws from Philox
+# stream_key = b (the engine's mv_set_state_streams(e, 1, 0)) instead of every state sharing
+# the seed's draws.  A state's success probability is unchanged; the run's success rate
+# becomes a sum of independent per-state outcomes, so its spread over seeds falls from
+# ~5 pp (shared draws: every state moves with the seed) to ~1.4 pp on botnet, which is
+# what lets the e2e test resolve 1 pp.
+for _k in list(CONFIGS):
+    CONFIGS[_k + "_ps"] = CONFIGS[_k]
 SEED0 = 100
 
 _P = None
@@ -54,13 +63,14 @@ def _init(project):
 
 
 def one_state(args):
-    s, b, n_gen, n_pop, n_off, seed, eps, thr = args
+    s, b, n_gen, n_pop, n_off, seed, eps, thr, per_state = args
     from oracle import moeva_oracle as mo
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
 
     p = _P
     ref = energy_ref_dirs(3, n_pop, seed=1)
-    r = mo.run_attack(p.problem(p.x[b], norm=2), ref, n_gen, n_pop + 3, n_off, seed)
+    r = mo.run_attack(p.problem(p.x[b], norm=2), ref, n_gen, n_pop + 3, n_off, seed,
+                      stream_key=b if per_state else 0)
     x_f = mo.genetic_to_ml(p.lay, r.pop_X, p.x[b])
     sc, mn = p.ml
     obj = mo.objectives_calc(p.x[b], x_f, p.constraints, p.types, sc, mn, p.weights, p.biases,
@@ -71,6 +81,7 @@ def one_state(args):
 
 def _save(out, name, project, B, n_gen, n_pop, n_off, eps, thr, seeds, resp, best, secs):
     np.savez_compressed(out, project=project, n_states=B, n_gen=n_gen, n_pop=n_pop,
+                        state_streams=name.endswith("_ps"),
                         n_offsprings=n_off, eps=eps, thr=thr, seeds=np.asarray(seeds),
                         respected=resp, best_f1=best, success_rate=resp.mean(axis=1),
                         evaluation_order="numpy (oracle.moeva_oracle.evaluate)",
@@ -92,7 +103,8 @@ def main(name, n_seeds):
     procs = int(os.environ.get("E2E_PROCS", os.cpu_count()))
     t0 = time.time()
     pend = {s: [np.zeros((B, 7), bool), np.zeros(B), 0, None] for s in todo}
-    jobs = [(s, b, n_gen, n_pop, n_off, s, eps, thr) for s in todo for b in range(B)]
+    per_state = name.endswith("_ps")
+    jobs = [(s, b, n_gen, n_pop, n_off, s, eps, thr, per_state) for s in todo for b in range(B)]
     with get_context("spawn").Pool(procs, initializer=_init, initargs=(project,)) as pool:
         for s, b, r, f1 in pool.imap_unordered(one_state, jobs):
             e = pend[s]
