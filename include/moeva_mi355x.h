@@ -202,9 +202,10 @@ typedef struct mv_attack_params {
 /* Whole attack on device: init population + evaluate + (n_gen-1) x {select, vary+evaluate,
  * survive}, no host round trip.  Asynchronous on `stream`.  Replaces Moeva2.generate's
  * per-state pymoo.minimize calls (moeva2.py:128-171, 194-205) for ALL bound states.
- * Two schedules, identical results: the per-phase kernel chain (k_gen, k_cons, k_mlp2,
- * k_survive per generation, state groups on up to 4 streams) and, for the shipped problem
- * layouts, ONE launch (k_attack: one workgroup per state runs every generation). */
+ * Schedule: per generation the row kernel (k_genc for wide IDENT rows such as botnet,
+ * k_narrow for LCLD-shaped rows, else k_gen + k_cons), the classifier (k_mlp2 / k_mlpw /
+ * k_mlp) and k_survive (survival + the next tournament), the states split into up to 4
+ * groups, each chain on its own stream. */
 int mv_attack_run(mv_engine* e, const mv_attack_params* params, void* stream);
 /* 0: auto (default), 1: per-phase kernel chain -- the same schedule.  2 (the retired
  * whole-attack kernel, measured slower than the chain) is rejected with MV_ERR_ARG. */
@@ -230,14 +231,16 @@ int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
 /* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
 int mv_attack_history(mv_engine* e, double* hist, void* stream);
-/* Per-kernel timing of the last mv_attack_run when enabled: HIP events recorded on the
- * run's stream around k_gen, k_cons, k_mlp2 and k_survive of every generation (summed ms). */
+/* Per-kernel timing of the last mv_attack_run when enabled (one state group then): HIP
+ * events recorded on the run's stream around the row kernel(s), the classifier and
+ * k_survive of every generation (summed ms). */
 int mv_set_profiling(mv_engine* e, int32_t enabled);
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations);
-/* Same events, split by kernel: ms[0] k_gen (variation + ML row + f2), ms[1] k_cons
- * (constraints + f3), ms[2] k_mlp (classifier, f1), ms[3] k_survive (survival + next
- * tournament), summed over the profiled generations. */
+/* Same events, split by kernel: ms[0] the row kernel's variation part (k_gen; k_genc or
+ * k_narrow: the whole row kernel), ms[1] k_cons (constraints + f3; 0 when k_genc or k_narrow
+ * ran), ms[2] the classifier (f1), ms[3] k_survive (survival + next tournament), summed over
+ * the profiled generations. */
 int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
 /* The kernels an attack generation runs for its offspring rows under the engine's current
  * options: 0 = k_gen then k_cons, 1 = k_narrow (one lane per row, both in one launch; the
@@ -246,8 +249,8 @@ int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
 int mv_get_row_kernel(mv_engine* e, int32_t* kind);
 /* The classifier kernel an attack generation runs: 0 = k_mlp (one tile of rows per
  * workgroup, any widths), 1 = k_mlp2 reading the child genes (no fp32 ML row is written),
- * 2 = k_mlp2 reading the fp32 ML rows, 3 = k_mlp2x (k_mlp2 with layer 0 fed by an LDS-DMA
- * ring of the fp32 ML rows), 4 = k_mlpw (bf16 weights), -1 = no device classifier.
+ * 2 = k_mlp2 reading the fp32 ML rows, 4 = k_mlpw (bf16 weights), -1 = no device classifier
+ * (3, the retired k_mlp2x, is no longer returned).
  * Lets a profiler price the ML-row bytes of the row kernel and the classifier. */
 int mv_get_mlp_kernel(mv_engine* e, int32_t* kind);
 

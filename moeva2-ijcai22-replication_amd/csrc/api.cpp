@@ -378,14 +378,9 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     // k_mlp2 packing of the hidden layers: Wp[kg][n][16] = W[16 kg + i][n] (zero padded)
     p.mlp2 = 1;
     for (int l = 1; l < md->n_layers; ++l) p.mlp2 &= md->dims[l] % 16 == 0 && md->dims[l] <= 128;
-    // xml_direct (k_mlp2 builds its layer-0 tiles from the child genes) unless k_mlp2x
-    // runs (MV_MLPX=1, A/B only: that pipeline DMAs the fp32 rows k_genc writes, xml, into
-    // LDS; slower end to end); MV_XML: the xml rows + k_mlp2
-    {
-      const char* mx = std::getenv("MV_MLPX");
-      p.mlpx = mx && mx[0] == '1' && mlpx_ok(p);
-      p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML") && !p.mlpx;
-    }
+    // xml_direct: k_mlp2 builds its layer-0 tiles from the child genes (MV_XML: the fp32
+    // ML rows written by the row kernel + k_mlp2, A/B only)
+    p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML");
     for (int l = 0; l + 1 < md->n_layers && p.mlp2; ++l) {
       const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
       const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major

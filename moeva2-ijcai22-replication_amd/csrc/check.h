@@ -94,8 +94,8 @@ __device__ __forceinline__ T* chk_ptr(T* p, const T* lo, const T* hi, int code) 
     return hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, 8 * sizeof(int));              \
   }
 #else
-#define MV_IDX(i, n, code) (i)
-#define MV_PTR(p, lo, hi, code) (p)
+#define MV_IDX(i, n, code) (static_cast<void>(n), (i))
+#define MV_PTR(p, lo, hi, code) (static_cast<void>(lo), static_cast<void>(hi), (p))
 #define MV_CHECKS_ON 0
 #define MV_DEFINE_TAKE_CHECKS(name)                  \
   hipError_t name(int* out) {                        \

@@ -13,6 +13,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// MV_CLOCKS (development builds: `make variant NAME=clk DEFS=-DMV_CLOCKS=1`): the k_genc /
+// k_mlp2 / k_survive phase clocks behind MV_GEN_PHASES / MV_MLP_PHASES / MV_SURV_PHASES.
+// Compiled out of the product build, so its kernels carry no clock branches.
+#ifndef MV_CLOCKS
+#define MV_CLOCKS 0
+#endif
+
 namespace mv {
 
 constexpr int MAX_LAYERS = 6;
@@ -94,7 +101,6 @@ struct DProblem {
   // is mutable feature g), so k_gen writes no fp32 ML row: the xml hand-off (Dm4 * 4 B
   // written + read back per row) is gone
   int xml_direct;
-  int mlpx;  // the classifier runs k_mlp2x (MV_MLPX=1 and mlpx_ok; development A/B)
 };
 
 struct DStates {
@@ -137,7 +143,7 @@ struct RowsArgs {
   int do_eval;              // 0: variation only
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
   long long* gphase;        // development (MV_GEN_PHASES): k_genc clocks [grid][8], or NULL
-  long long* mphase;        // development (MV_MLP_PHASES): k_mlp2 / k_mlp2x clocks [grid][8]
+  long long* mphase;        // development (MV_MLP_PHASES): k_mlp2 clocks [grid][8]
 };
 
 // Survival ------------------------------------------------------------------------------

@@ -113,11 +113,7 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   preload();
   // (1) mutation positions and their PM uniforms
   const float lq = __log2f(1.0f - 1.0f / (float)V);
-#ifdef MV_DBG_NOMUT
-  bool going = false;  // development: prologue cost without mutations (results wrong)
-#else
   bool going = mine && !sbx;
-#endif
   int pos = -1, cnt = 0, ovf = 0;
   double mu[CAP] = {};
 #pragma unroll 1
@@ -255,7 +251,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 1] = clock64();
+  if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 1] = clock64();
   const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
   const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
   const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
@@ -306,7 +302,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (mine) par_v = irow | (irow << 16);
     preload();
   }
-  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 2] = clock64();
+  if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 2] = clock64();
   const bool l2 = p.norm == 2;
   // child genes -> pool, fp32 ML row, f2 (row k of this wave, genes already mutated)
   auto finish_row = [&](int k, const double* x) {
@@ -497,7 +493,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
+  if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
   double* xrow = (double*)(smem + o.a_end + o.x_end + wave * o.rb);
   {
     const double* s_xi = (const double*)(smem + o.a_end + o.xi);
@@ -592,19 +588,19 @@ __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
-  if (a.gphase && threadIdx.x == 0) {
+  if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 0] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 6] = wall_clock64();
   }
   const int orow_v = gen_rows<IDENT, NT, SBX>(a, gen, hist_row0, rows_wg, smem);
-  if (a.gphase && threadIdx.x == 0) a.gphase[(size_t)blockIdx.x * 8 + 3] = clock64();
+  if (MV_CLOCKS && a.gphase && threadIdx.x == 0) a.gphase[(size_t)blockIdx.x * 8 + 3] = clock64();
   // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
   // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them.  Both
   // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   cons_rows<false, IDENT, NT>(a, hist_row0, rows_wg, smem, true, orow_v);
-  if (a.gphase && threadIdx.x == 0) {
+  if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 7] = wall_clock64();
   }
@@ -969,7 +965,7 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
       *(float4*)(A0 + (buf) * M2_ROWS * M2_ALD + row * M2_ALD + 4 * q) = v;               \
     }                                                                                    \
   }
-    const bool ph = a.mphase && tid == 0 && tile == (int)blockIdx.x;
+    const bool ph = MV_CLOCKS && a.mphase && tid == 0 && tile == (int)blockIdx.x;
     long long* phq = a.mphase + (size_t)blockIdx.x * 16;
     if (ph) {
       phq[0] = clock64();
@@ -1276,235 +1272,6 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
         if (a.hist)
           a.hist[((size_t)s * a.hist_rows + MV_IDX(hist_row0 + i, a.hist_rows, CK_MLP_OUT)) *
                  a.hist_w] = f1;
-      }
-    }
-    if (ph) {
-      phq[5] = clock64();
-      phq[7] = wall_clock64();
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// k_mlp2x: k_mlp2 (fp32, 64-row tiles, the same MFMA operand layout and k order, so f1 is
-// bit-identical) with layer 0 fed by an LDS-DMA ring.  A launch of one state group has fewer
-// tiles than CUs, so its duration is ONE tile's latency, and k_mlp2 paid its layer-0 chunks
-// one HBM round trip at a time (one chunk of register lookahead, no registers left for
-// more: ~60 us per launch in the 4-group schedule for ~8 us of MFMA work).  Here each of the
-// seven 64-k chunks -- the tile's fp32 ML rows (xml, written by k_genc) and the packed
-// layer-0 weights for those k -- is moved by global_load_lds (inline asm: hipcc neither
-// counts it nor inserts vmcnt(0) before the LDS reads) into a ring of MX_NR slots up to
-// MX_NR chunks ahead; the MFMAs read A and B from LDS, and the loop waits with counted
-// vmcnt(N) and raw barriers, never vmcnt(0) while later chunks are in flight.
-// A chunk image: 64 rows x 16 pieces of 16 B, piece q of row R stored at position
-// q ^ (R & 15) (the source address carries the swizzle: a DMA writes its 1 KiB lane-linear),
-// so one MFMA A read -- rows il of a 16-row tile, piece 4 g + ka -- hits 16 bank groups.
-// One global_load_lds_dwordx4: 16 B per lane from gsrc to the wave-uniform LDS byte address
-// lds_dst + 16 lane (M0 saved and restored inside the statement: it is compiler-reserved).
-__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
-  unsigned keep;
-  const unsigned dst = __builtin_amdgcn_readfirstlane(lds_dst);  // wave-uniform by construction
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(dst)
-               : "memory");
-}
-
-template <int CJ, int NR>
-__global__ __launch_bounds__(256, 1) void k_mlp2x(int slot, int hist_row0) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const RowsArgs& a = c_rows[slot];
-  const DProblem& p = a.p;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int il = lane & 15, ka = lane >> 4;
-  const int nl = p.n_layers;
-  const int K0 = p.Dm4, N0 = p.dims[1];
-  const int hld = mlp2_hmax(p) + 4;
-  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
-  int* rowst = (int*)smem;
-  float* wl = (float*)(smem + 256);
-  float* bl = wl + Klast * nout;
-  for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
-  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
-  unsigned char* ring = smem + mlpx_ring_at(p);
-  const size_t slotb = mlpx_slot(p);
-  float* H = (float*)ring;  // hidden ping-pong + final partial sums: the ring after layer 0
-  float* part = H + 2 * M2_ROWS * hld;
-  const unsigned ring_lds = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)ring);
-  const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
-  const int nkg0 = K0 >> 4;
-  const int nch = (nkg0 + 3) >> 2;
-  const float* Wp0 = p.Wp[0];
-  const unsigned wbytes = 4u * N0 * 64;  // one chunk's weights: 4 k-groups x N0 x 16 fp32
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int r0 = tile * M2_ROWS;
-    __syncthreads();  // the previous tile's readers of rowst / H / ring are done
-    if (tid < M2_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
-    // chunk c into ring slot sl (see above); pieces past the row's K0 re-read its first
-    // piece, weight pieces past the last k-group re-read k-group 0 (in bounds, never used)
-#define MX_DMA(c, sl)                                                                     \
-  {                                                                                       \
-    const unsigned sbase = ring_lds + (unsigned)((sl) * slotb);                           \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                       \
-      const int row = wave * 16 + 4 * q + (lane >> 4);                                    \
-      const int qs = (lane & 15) ^ (row & 15);                                            \
-      const int rr = r0 + row < a.total ? r0 + row : a.total - 1;                         \
-      const int k = (c) * 64 + 4 * qs;                                                    \
-      glds16_asm(a.xml + (size_t)rr * K0 + (k < K0 ? k : 0),                              \
-                 sbase + (unsigned)(wave * 16 + 4 * q) * 256u);                           \
-    }                                                                                     \
-    _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                       \
-      const unsigned off = (unsigned)(wave + 4 * q) * 1024u + (unsigned)lane * 16u;       \
-      const unsigned kgl = off / (unsigned)(N0 * 64);                                     \
-      const unsigned goff = 4u * (c) + kgl < (unsigned)nkg0 ? (unsigned)(c) * wbytes + off \
-                                                            : off % (unsigned)(N0 * 64);  \
-      glds16_asm((const unsigned char*)Wp0 + goff,                                        \
-                 sbase + M2_ROWS * 64 * 4 + (unsigned)(wave + 4 * q) * 1024u);            \
-    }                                                                                     \
-  }
-    const bool ph = a.mphase && tid == 0 && tile == (int)blockIdx.x;
-    long long* phq = a.mphase + (size_t)blockIdx.x * 16;
-    if (ph) {
-      phq[0] = clock64();
-      phq[6] = wall_clock64();
-    }
-    for (int c = 0; c < NR && c < nch; ++c) MX_DMA(c, c)
-    if (ph) phq[1] = clock64();
-    floatx4 acc[CJ][4];
-#pragma unroll
-    for (int cj = 0; cj < CJ; ++cj)
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const TileMap m = tile_map(N0 >> 4, wave);
-    const int nct0 = N0 >> 4;
-    for (int c = 0; c < nch; ++c) {
-      // chunk c landed: this wave's loads for it are older than the <= NR - 1 younger
-      // chunks' MX_DMA_PER_CHUNK each (vmcnt retires in order); the barrier makes every
-      // wave's share visible
-      const int after = min(NR - 1, nch - 1 - c);
-      if (after >= 3)
-        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else if (after == 2)
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (after == 1)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (ph && c == 0) phq[2] = clock64();
-      const float* As = (const float*)(ring + (size_t)(c % NR) * slotb);
-      const float* Ws = As + M2_ROWS * 64;
-      const int ng = min(4, nkg0 - 4 * c);
-      for (int g = 0; g < ng; ++g) {
-        float4 bf[CJ], af[4];
-#pragma unroll
-        for (int cj = 0; cj < CJ; ++cj) {
-          const int ct = m.cb + 4 * cj < nct0 ? m.cb + 4 * cj : nct0 - 1;
-          bf[cj] = *(const float4*)(Ws + ((g * N0 + ct * 16 + il) * 16 + 4 * ka));
-        }
-#pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          const int R = (m.rt0 + (rt < m.nrt ? rt : 0)) * 16 + il;
-          af[rt] = *(const float4*)(As + R * 64 + (((4 * g + ka) ^ il) << 2));
-        }
-        mfma_k4<CJ>(af, bf, acc, m.cb, nct0, m.nrt);
-      }
-      // every wave is done reading the slot before it is refilled
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (c + NR < nch) MX_DMA(c + NR, c % NR)
-    }
-#undef MX_DMA
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // the ring is free: H aliases it
-    if (ph) phq[3] = clock64();
-    // hidden layers: layer l writes H[l & 1] (k_mlp2's code)
-    for (int l = 0; l + 1 < nl; ++l) {
-      const int N = p.dims[l + 1];
-      const TileMap mm = tile_map(N >> 4, wave);
-      if (l > 0) {
-#pragma unroll
-        for (int cj = 0; cj < CJ; ++cj)
-#pragma unroll
-          for (int rt = 0; rt < 4; ++rt) acc[cj][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
-        mlp2_layer<CJ>(H + ((l - 1) & 1) * M2_ROWS * hld, hld, p.Wp[l], p.dims[l] >> 4, N, acc,
-                       mm, il, ka);
-      }
-      float* out = H + (l & 1) * M2_ROWS * hld;
-#pragma unroll
-      for (int cj = 0; cj < CJ; ++cj) {
-        const int ct = mm.cb + 4 * cj;
-        if (ct < (N >> 4)) {
-          const int col = ct * 16 + il;
-#pragma unroll
-          for (int rt = 0; rt < 4; ++rt) {
-            if (rt >= mm.nrt) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int row = (mm.rt0 + rt) * 16 + ka * 4 + j;
-              float bv;
-              if (l == 0) {
-                const int st = rowst[row];
-                bv = a.s.bias1[(size_t)(st < 0 ? 0 : st) * N0 + col];
-              } else {
-                bv = p.bias[l][col];
-              }
-              const float v = acc[cj][rt][j] + bv;
-              out[row * hld + col] = v > 0.f ? v : 0.f;
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-    if (ph) phq[4] = clock64();
-    // final Dense + softmax -> f1 (k_mlp2's quarters and combination order)
-    {
-      const int kq = Klast >> 2;
-      const float* ir = H + ((nl - 2) & 1) * M2_ROWS * hld + lane * hld + wave * kq;
-      const float* wq = wl + wave * kq * nout;
-      float ps[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) ps[c] = 0.f;
-      for (int k = 0; k < kq; k += 4) {
-        const float4 v = *(const float4*)(ir + k);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          if (c < nout) {
-            ps[c] = fmaf(v.x, wq[k * nout + c], ps[c]);
-            ps[c] = fmaf(v.y, wq[(k + 1) * nout + c], ps[c]);
-            ps[c] = fmaf(v.z, wq[(k + 2) * nout + c], ps[c]);
-            ps[c] = fmaf(v.w, wq[(k + 3) * nout + c], ps[c]);
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (c < nout) part[(wave * M2_ROWS + lane) * nout + c] = ps[c];
-    }
-    __syncthreads();
-    if (tid < M2_ROWS) {
-      const int st = rowst[tid];
-      if (st >= 0) {
-        double z[8];
-        double mx = -__builtin_inf();
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          z[c] = 0.0;
-          if (c < nout) {
-            const float* q = part + tid * nout + c;
-            z[c] = (double)((((q[0] + q[M2_ROWS * nout]) + q[2 * M2_ROWS * nout]) +
-                             q[3 * M2_ROWS * nout]) + bl[c]);
-            mx = z[c] > mx ? z[c] : mx;
-          }
-        }
-        const double f1 = softmax_pick(z, nout, mx, a.s.min_class[st]);
-        const int i = r0 + tid - st * a.n;
-        if (a.F) {
-          const int orow = a.out_map ? a.out_map[(size_t)st * a.n + i] : i;
-          a.F[((size_t)st * a.out_rows + orow) * 3] = f1;
-        }
-        if (a.hist) a.hist[((size_t)st * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
       }
     }
     if (ph) {
@@ -2201,38 +1968,10 @@ static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   return hipGetLastError();
 }
 
-static hipError_t mlpx_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
-  static bool configured = false;
-  if (!configured) {
-    allow_lds(k_mlp2x<1, 2>);
-    allow_lds(k_mlp2x<1, 3>);
-    allow_lds(k_mlp2x<1, 4>);
-    configured = true;
-  }
-  static const int nr = [] {  // ring depth (MV_MLPX_NR, development A/B)
-    const char* v = std::getenv("MV_MLPX_NR");
-    const int n = v ? std::atoi(v) : MX_NR;
-    return n < 2 ? 2 : n > 4 ? 4 : n;
-  }();
-  const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
-  const int per_cu = (int)((160 * 1024) / mlpx_lds(a.p, nr));
-  const int cap = cu_count() * (per_cu < 1 ? 1 : per_cu);
-  const int grid = ntiles < cap ? ntiles : cap;
-  const size_t lds = mlpx_lds(a.p, nr);
-  if (nr == 2)
-    hipLaunchKernelGGL((k_mlp2x<1, 2>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
-  else if (nr == 3)
-    hipLaunchKernelGGL((k_mlp2x<1, 3>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
-  else
-    hipLaunchKernelGGL((k_mlp2x<1, 4>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
-  return hipGetLastError();
-}
-
 // launch_mlp's choice for a problem: 0 k_mlp, 1 k_mlp2 reading the genes (xml_direct),
-// 2 k_mlp2 reading the fp32 ML rows, 3 k_mlp2x, 4 k_mlpw (bf16), -1 no model
+// 2 k_mlp2 reading the fp32 ML rows, 4 k_mlpw (bf16), -1 no model (3, k_mlp2x, was retired)
 int mlp_kernel_kind(const DProblem& p) {
   if (p.n_layers == 0) return -1;
-  if (p.mlpx && !p.mlp_bf16) return 3;
   if (p.mlp2 && !std::getenv("MV_MLP_V1") && !(p.mlp_bf16 && std::getenv("MV_MLPW")))
     return p.xml_direct ? 1 : 2;
   if (p.mlp_bf16 && mlpw_lds(p).total <= 160 * 1024 && !std::getenv("MV_MLPW_OFF")) return 4;
@@ -2241,9 +1980,6 @@ int mlp_kernel_kind(const DProblem& p) {
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
-  // MV_MLPX=1 (api.cpp sets p.mlpx and turns xml_direct off, so k_genc writes the fp32
-  // rows): the LDS-DMA pipeline
-  if (a.p.mlpx && !a.p.mlp_bf16) return mlpx_go(a, slot, hist_row0, stream);
   // (MV_MLPW=1: the bf16 mode runs k_mlpw for narrow nets too -- development A/B)
   if (a.p.mlp2 && !std::getenv("MV_MLP_V1") && !(a.p.mlp_bf16 && std::getenv("MV_MLPW"))) {
     if (a.p.mlp_bf16)

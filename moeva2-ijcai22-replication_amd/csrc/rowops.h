@@ -575,29 +575,6 @@ __host__ __device__ inline size_t mlp2_lds(const DProblem& p) {
   return mlp2_sc_off(p) + (p.xml_direct ? (size_t)2 * p.Dm4 * 8 : 0);
 }
 
-// k_mlp2x (eval.hip): the LDS-DMA ring of layer-0 chunks
-constexpr int MX_NR = 4;
-constexpr int MX_DMA_PER_CHUNK = 8;  // global_load_lds per wave per chunk: 4 A + 4 W (N0 = 64)
-
-__host__ __device__ inline size_t mlpx_ring_at(const DProblem& p) {
-  return (mlp2_head(p) + 1023) & ~(size_t)1023;
-}
-__host__ __device__ inline size_t mlpx_slot(const DProblem& p) {
-  return (size_t)M2_ROWS * 64 * 4 + (size_t)4 * p.dims[1] * 16 * 4;
-}
-__host__ __device__ inline size_t mlpx_lds(const DProblem& p, int nr = MX_NR) {
-  const size_t ring = nr * mlpx_slot(p);
-  const size_t h = (size_t)2 * M2_ROWS * (mlp2_hmax(p) + 4) * 4 +
-                   (size_t)4 * M2_ROWS * p.dims[p.n_layers] * 4;
-  return mlpx_ring_at(p) + (ring > h ? ring : h);
-}
-// k_mlp2x's shape: fp32 xml rows, first hidden width 64 (4 weight DMAs per wave per chunk),
-// the k_mlp2 limits on the other widths
-__host__ __device__ inline bool mlpx_ok(const DProblem& p) {
-  return p.mlp2 && p.n_layers >= 2 && p.dims[1] == 64 && mlp2_hmax(p) <= 64 &&
-         (p.dims[p.n_layers - 1] & 15) == 0 && mlpx_lds(p) <= 160 * 1024;
-}
-
 // A wave's share of a layer's (column tile, row tile) grid: column tiles cb + 4cj over all
 // four row tiles when the layer has >= 3 column tiles, else the waves also split the row
 // tiles (N = 32: two waves per column tile, N = 16: one row tile per wave).

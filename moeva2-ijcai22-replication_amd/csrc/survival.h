@@ -345,7 +345,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   const double pre_worst = tid < 3 ? a.worst[(size_t)b * 3 + tid] : 0.0;
   const bool slot_mode = a.pop_slot != nullptr;
 #define PHASE(k) \
-  if (a.phase && tid == 0) a.phase[(size_t)b * 32 + (k)] = clock64();
+  if (MV_CLOCKS && a.phase && tid == 0) a.phase[(size_t)b * 32 + (k)] = clock64();
   PHASE(0)
 
   // ---- load merged F, ref points
@@ -899,7 +899,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     // 1000, where the aspiration directions crowd together and 72 of 303 individuals per
     // state have more pre-filter candidates than the fast pass keeps.
     const int n_flag = L.iscal[15];
-    if (a.phase && tid == 0) a.phase[(size_t)b * 32 + 12] = n_flag;
+    if (MV_CLOCKS && a.phase && tid == 0) a.phase[(size_t)b * 32 + 12] = n_flag;
     for (int t = wave; t < n_flag; t += T / 64) {
       const int p = L.key[t];
       const int m = L.I[p];

@@ -90,7 +90,7 @@ def _e2e(fixture):
 DEVICE_SEEDS = list(range(1000, 1032))  # disjoint from make_e2e_seeds.py's SEED0 = 100 + k
 
 
-def _device_seed_rates(name, B, n_gen, n_pop, n_off, eps, thr, seeds):
+def _device_seed_rates(name, B, n_gen, n_pop, n_off, eps, thr, seeds, state_streams=False):
     """Device attack at every seed, scored like 04_moeva.py:112-131: final populations
     decoded on the device (FeatureEncoder.genetic_to_ml) and scored by the package's
     ObjectiveCalculator (objective_calculator.py:44-119, pinned by
@@ -111,6 +111,7 @@ def _device_seed_rates(name, B, n_gen, n_pop, n_off, eps, thr, seeds):
     eng = get_engine(c, Classifier(model), scaler, 2)
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    eng.set_state_streams(state_streams, 0)
     calc = ObjectiveCalculator(Classifier(model), c, 1, {"f1": thr, "f2": eps},
                                min_max_scaler=scaler, ml_scaler=scaler, norm=2)
     oc, ceng, mlp = calc._device()
@@ -203,3 +204,48 @@ def test_success_rate_within_1pp_at_full_config(fixture):
     sr_dev, sr_ref, best, best_ref = _e2e(fixture)
     assert np.all(np.abs(sr_dev - sr_ref) <= 0.01 + 1e-12), (sr_dev, sr_ref)
     assert abs(best.mean() - best_ref.mean()) <= 0.01
+
+
+DEVICE_SEEDS_PS = list(range(2000, 2064))  # disjoint from make_e2e_seeds.py's SEED0 = 100 + k
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("fixture", ["e2e_botnet_rq1_ps_seeds.npz",
+                                     "e2e_lcld_rq1_g100_ps_seeds.npz"])
+def test_success_rate_within_1pp_state_streams(fixture):
+    """north_star's +-1 pp, resolved.  Both sides run with PER-STATE random streams (state b
+    draws from Philox stream b: the oracle's run_attack(stream_key=b), the engine's
+    mv_set_state_streams(e, 1, 0)).  A state's success probability is the same as with the
+    reference's shared draws; the states' outcomes become independent, so a run's success
+    rate spreads ~1.4 pp over seeds on botnet instead of ~5 pp, and the comparison of the
+    seed means can resolve 1 pp: for every o_k, |mean(device) - mean(oracle)| <= 1 pp AND
+    the 99 % two-sample t half-width of that difference is <= 1.5 pp (so a 2.5 pp gap
+    cannot pass).  The oracle side (tests/golden/make_e2e_seeds.py <config>_ps) is the
+    numpy-order restatement of the reference's arithmetic; 64 device seeds."""
+    path = os.path.join(GOLD, fixture)
+    if not os.path.exists(path):
+        pytest.skip(f"{fixture} not generated (tests/golden/make_e2e_seeds.py)")
+    d = np.load(path, allow_pickle=False)
+    assert bool(d["state_streams"])
+    name = str(d["project"])
+    B, G = int(d["n_states"]), int(d["n_gen"])
+    thr, eps = float(d["thr"]), float(d["eps"])
+    _, _, resp, _ = _device_seed_rates(name, B, G, int(d["n_pop"]), int(d["n_offsprings"]),
+                                       eps, thr, DEVICE_SEEDS_PS, state_streams=True)
+    sr_dev = resp.mean(axis=1)
+    sr_ref = np.asarray(d["success_rate"], np.float64)
+    assert sr_ref.shape[0] >= 6
+    diff = sr_dev.mean(axis=0) - sr_ref.mean(axis=0)
+    half = _t_bound(sr_dev, sr_ref)
+    np.set_printoptions(linewidth=200)
+    print(f"\n{fixture}: {sr_ref.shape[0]} oracle seeds, {sr_dev.shape[0]} device seeds "
+          "(per-state streams)")
+    print("  oracle o1..o7 mean", np.round(sr_ref.mean(axis=0), 4), "sd",
+          np.round(sr_ref.std(axis=0, ddof=1), 4))
+    print("  device o1..o7 mean", np.round(sr_dev.mean(axis=0), 4), "sd",
+          np.round(sr_dev.std(axis=0, ddof=1), 4))
+    print("  diff", np.round(diff, 4), "99% t half-width", np.round(half, 4))
+    print("  oracle per seed o4", np.round(sr_ref[:, 3], 4))
+    print("  device per seed o4", np.round(sr_dev[:, 3], 4))
+    assert np.all(half <= 0.015 + 1e-12), half
+    assert np.all(np.abs(diff) <= 0.01 + 1e-12), (diff, half)

@@ -578,22 +578,6 @@ def test_narrow_rows_match_wave_kernels(monkeypatch, name, B, P, O, G, hist, nor
     np.testing.assert_array_equal(h1.cpu().numpy(), h0.cpu().numpy())
 
 
-@pytest.mark.parametrize("name,B,P,O,G,hist", [
-    ("botnet", 9, 203, 100, 5, 2), ("botnet_augmented", 3, 43, 20, 6, 1),
-    ("botnet", 4, 643, 320, 3, 2), ("lcld", 7, 43, 20, 5, 2)])
-def test_mlp_dma_ring_matches_k_mlp2(monkeypatch, name, B, P, O, G, hist):
-    """k_mlp2x (layer 0 fed from an LDS-DMA ring, same MFMA operand layout and k order) is
-    bit-identical to k_mlp2 reading the ML rows directly: genes, F and the full history."""
-    X = Project(name).x[:B]
-    monkeypatch.setenv("MV_MLPX", "1")
-    _, g1, F1, h1, _ = _attack(name, X, G, 23, hist=hist, P=P, O=O, mode="chain")
-    monkeypatch.setenv("MV_MLPX", "0")
-    _, g0, F0, h0, _ = _attack(name, X, G, 23, hist=hist, P=P, O=O, mode="chain")
-    np.testing.assert_array_equal(g1.cpu().numpy(), g0.cpu().numpy())
-    np.testing.assert_array_equal(F1.cpu().numpy(), F0.cpu().numpy())
-    np.testing.assert_array_equal(h1.cpu().numpy(), h0.cpu().numpy())
-
-
 def test_attack_invariants_lcld():
     """Whole device loop: bounds, integrality, F == re-evaluation, history layout.  (Each
     generation's kernels are pinned bit-exactly above; the loop is compared end to end
