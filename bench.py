@@ -167,10 +167,19 @@ def _cpu_state(args):
     return n_pop + 3 + (gens - 1) * n_off
 
 
+def cpu_affinity() -> int:
+    """CPUs in this process's affinity mask (os.sched_getaffinity)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_cores():
-    """Host cores this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on
-    the GPU box; os.cpu_count() there reports the whole machine), else os.cpu_count()."""
-    n = os.cpu_count() or 1
+    """Host cores the baseline uses: the process's affinity mask, capped by the box's CPU
+    share (OMP_NUM_THREADS is set to it on the GPU box, whose affinity mask and
+    os.cpu_count() cover the whole machine)."""
+    n = cpu_affinity()
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit() and int(env) > 0:
         n = min(n, int(env))
@@ -196,7 +205,10 @@ def cpu_baseline(w, sample_gens=100, cores=None):
     return {"value": n_eval / dt, "unit": "evals/s", "cores": cores, "kind": "port",
             "sample": f"{cores} {w['project']} states x {sample_gens} generations "
                       f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack (numpy), one "
-                      f"process per core, os.cpu_count()={os.cpu_count()}",
+                      f"process per core; affinity mask {cpu_affinity()} CPUs, box CPU "
+                      f"share (OMP_NUM_THREADS) {os.environ.get('OMP_NUM_THREADS', 'unset')}, "
+                      f"os.cpu_count()={os.cpu_count()}",
+            "affinity_cpus": cpu_affinity(),
             "seconds": dt}
 
 

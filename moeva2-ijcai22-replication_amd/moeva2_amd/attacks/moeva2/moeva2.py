@@ -43,12 +43,25 @@ def _non_dominated(F):
     return ~dominated
 
 
+def _shard_offset(n_states, group=None) -> int:
+    """Global index of this rank's first state under moeva2_amd.distributed's sharding (0
+    without a process group): the per-state random streams are keyed by it."""
+    import torch.distributed as dist
+
+    from ...distributed import shard_bounds
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0
+    return shard_bounds(n_states, dist.get_world_size(group), dist.get_rank(group))[0]
+
+
 class Moeva2:
     def __init__(self, classifier_path: str, constraints: Constraints, ml_scaler=None,
                  problem_class=None, l2_ball_size=0.1, norm=np.inf, n_gen=625, n_pop=640,
                  n_offsprings=320, scale_objectives=True, save_history=False, seed=None,
                  n_jobs=-1, verbose=1, device: int = 0, crossover: str = "two_point",
-                 sbx_eta: float = 30.0, mlp_dtype: str = "fp32") -> None:
+                 sbx_eta: float = 30.0, mlp_dtype: str = "fp32",
+                 state_streams: bool = False) -> None:
         self._classifier_path = classifier_path
         self._constraints = constraints
         self._ml_scaler = ml_scaler
@@ -77,6 +90,10 @@ class Moeva2:
         if mlp_dtype not in ("fp32", "bf16"):
             raise ValueError(f"mlp_dtype must be 'fp32' or 'bf16', got {mlp_dtype!r}")
         self._mlp_dtype = mlp_dtype
+        # engine extension: per-state random streams (state b draws from Philox stream b of
+        # the global state order) instead of the reference's shared draws -- the same attack
+        # per state, independent outcomes across states (mv_set_state_streams)
+        self._state_streams = bool(state_streams)
         self._classifier = None
         self.last_engine = None
 
@@ -95,7 +112,7 @@ class Moeva2:
         """RNSGA3: n_ref_points * n_aspiration_dirs (1) + n_obj."""
         return self._n_pop + N_OBJ
 
-    def generate(self, x: np.ndarray, minimize_class, return_device=False):
+    def generate(self, x: np.ndarray, minimize_class, return_device=False, first_state=0):
         if isinstance(minimize_class, (int, np.integer)):
             minimize_class = np.repeat(minimize_class, x.shape[0])
         minimize_class = np.asarray(minimize_class)
@@ -116,6 +133,7 @@ class Moeva2:
                          self._scale_objectives, self.device)
         eng.set_crossover(self._crossover, self._sbx_eta)
         eng.set_mlp_precision(self._mlp_dtype)
+        eng.set_state_streams(self._state_streams, first_state)
         bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
         xl = np.array([b[0] for b in bounds], np.float64)
         xu = np.array([b[1] for b in bounds], np.float64)
@@ -160,10 +178,41 @@ class Moeva2:
         from ...distributed import generate_sharded
 
         def attack(xs, mcs):
-            genes, F, _ = self.generate(xs, mcs, return_device=True)
+            genes, F, _ = self.generate(xs, mcs, return_device=True,
+                                        first_state=_shard_offset(x.shape[0], group))
             return genes, F
 
         return generate_sharded(attack, x, minimize_class, group, empty=self._empty_device)
+
+    def generate_scored_sharded(self, x: np.ndarray, minimize_class, objective_calculator,
+                                group=None):
+        """generate_sharded + the success evaluation of 04_moeva.py:112-131, with only the
+        verdict crossing the links: each rank attacks its slice, decodes its final
+        populations on its GPU (FeatureEncoder.genetic_to_ml), scores them with
+        ``objective_calculator`` (ObjectiveCalculator._calculate_objective on the device) and
+        all-gathers per-state o1..o7 flags plus one successful candidate per state
+        (moeva2_amd.distributed.success_flags).  Returns, on every rank, flags (B, 7) bool
+        (their column means are success_rate_3d's o1..o7) and best (B, D) (NaN rows: no
+        o7-successful candidate)."""
+        import torch
+
+        from ...distributed import generate_scored_sharded, success_flags
+
+        D = int(x.shape[1])
+        dev = torch.device("cuda", self.device)
+
+        def attack(xs, mcs):
+            genes, _, _ = self.generate(xs, mcs, return_device=True,
+                                        first_state=_shard_offset(x.shape[0], group))
+            xf = torch.empty((genes.shape[0], genes.shape[1], D), dtype=torch.float64,
+                             device=dev)
+            self.last_engine.decode(genes, xf)
+            xi = torch.from_numpy(np.ascontiguousarray(xs, np.float64)).to(dev)
+            obj = objective_calculator.calculate_objectives_device(xi, xf)
+            return success_flags(obj, xf, objective_calculator._thresholds)
+
+        flags, best = generate_scored_sharded(attack, x, minimize_class, D, group, dev)
+        return flags.cpu().numpy().astype(bool), best.cpu().numpy()
 
     def _empty_device(self):
         """Zero-state (genes, F) device tensors of this attack's shapes."""

@@ -115,6 +115,25 @@ class ObjectiveCalculator:
         assert not bool(bad.any().item()), "candidate or initial state outside the scaler range"
         return obj.cpu().numpy()
 
+    def calculate_objectives_device(self, x_initials, x):
+        """``calculate_objectives_3d`` on device tensors (engine extension, no host copy):
+        x_initials (B, D), x (B, n, D) fp64 on the GPU -> obj (B, n, 3) on the GPU.  Needs the
+        device constraint program and classifier (host plugins: calculate_objectives_3d)."""
+        import torch
+
+        oc, ceng, mlp = self._device()
+        if ceng is None or mlp is None:
+            raise ValueError("calculate_objectives_device needs the device constraint program "
+                             "and classifier; use calculate_objectives_3d for host plugins")
+        B, n = x.shape[0], x.shape[1]
+        obj = torch.empty((B, n, 3), dtype=torch.float64, device=x.device)
+        if B * n == 0:
+            return obj
+        bad = torch.empty((B, n), dtype=torch.int32, device=x.device)
+        oc.run(ceng, mlp, x_initials.contiguous(), x.contiguous(), self._minimize_class, obj, bad)
+        assert not bool(bad.any().item()), "candidate or initial state outside the scaler range"
+        return obj
+
     def _calculate_objective(self, x_initial, x_f):
         x_f = np.atleast_2d(x_f)
         return self.calculate_objectives_3d(np.asarray(x_initial)[None, :], x_f[None])[0]

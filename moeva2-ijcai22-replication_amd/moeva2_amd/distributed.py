@@ -6,6 +6,12 @@ state's result does not depend on which GPU runs it.  Rank r of a world of size 
 the contiguous slice [r*ceil(B/G), (r+1)*ceil(B/G)); no collective runs inside the
 generation loop; one all_gather (RCCL over xGMI on MI355X, gloo in the CPU tests) returns
 the per-state results to every rank.
+
+Two gathers are offered: ``generate_sharded`` returns the final populations of every state
+(genes + F: 271 MB per copy for the 387 botnet states), ``generate_scored_sharded`` scores
+each rank's own populations with the ObjectiveCalculator on its GPU first
+(``success_flags``) and gathers only what 04_moeva.py:112-131 keeps of them -- the per-state
+o1..o7 flags (uint8) and one successful candidate per state (D fp64) -- 2.3 MB for botnet.
 """
 from __future__ import annotations
 
@@ -66,3 +72,50 @@ def generate_sharded(attack: Callable, x: np.ndarray, minimize_class, group=None
     else:
         outs = empty()
     return tuple(all_gather_states(t, B, group) for t in outs)
+
+
+def success_flags(obj, x_f, thresholds):
+    """The ObjectiveCalculator verdict on one rank's final populations, computed where the
+    tensors live (the GPU in the product path).
+
+    obj (b, n, 3): per candidate [constraint violation, f1, f2] (objective_calculator.py:44-84);
+    x_f (b, n, D): the candidates in ML space.  Returns
+      flags (b, 7) uint8: o1..o7 of _objective_respected (:86-101) reached by at least one
+        candidate of the state (success_rate_3d's per-state "> 0", :121-128);
+      best (b, D) float64: the o7-successful candidate with the smallest f1 -- what
+        _get_one_successful(preferred_metrics="misclassification", max_inputs=1) keeps
+        (:153-182; equal f1: the lowest index) -- NaN where the state has none.
+    NaN objectives compare false, as in numpy."""
+    import torch
+
+    cv, f1, f2 = obj[..., 0], obj[..., 1], obj[..., 2]
+    c = cv <= 0
+    m = f1 < float(thresholds["f1"])
+    l = f2 <= float(thresholds["f2"])
+    resp = torch.stack([c, m, l, c & m, c & l, m & l, c & m & l], dim=-1)
+    b, n = obj.shape[0], obj.shape[1]
+    flags = resp.any(dim=1).to(torch.uint8) if n else torch.zeros((b, 7), dtype=torch.uint8,
+                                                                  device=obj.device)
+    D = x_f.shape[-1]
+    best = torch.full((b, D), float("nan"), dtype=torch.float64, device=x_f.device)
+    if b and n:
+        key = torch.where(resp[..., 6], f1, torch.full_like(f1, float("inf")))
+        idx = torch.argmin(key, dim=1)  # first minimal index
+        ok = flags[:, 6] != 0
+        rows = x_f[torch.arange(b, device=x_f.device), idx]
+        best[ok] = rows[ok].to(torch.float64)
+    return flags, best
+
+
+def generate_scored_sharded(attack_scored: Callable, x: np.ndarray, minimize_class, D: int,
+                            group=None, device=None):
+    """``generate_sharded`` for ``attack_scored(x_shard, mc_shard) -> (flags, best)`` (see
+    success_flags): only the per-state flags and successful candidates cross the links.
+    Returns (flags (B, 7) uint8, best (B, D) float64) on every rank, in state order."""
+    import torch
+
+    def empty():
+        return (torch.zeros((0, 7), dtype=torch.uint8, device=device),
+                torch.zeros((0, D), dtype=torch.float64, device=device))
+
+    return generate_sharded(attack_scored, x, minimize_class, group, empty=empty)

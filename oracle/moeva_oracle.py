@@ -576,6 +576,16 @@ def ref_dirs_from_points(ref_point, asp_dirs, mu):
             s = (rf[:, 0] + rf[:, 1]) + rf[:, 2]
             r[fix] = rf / s[:, None]
         return np.concatenate([r, np.eye(n_obj)])
+    return _ref_dirs_from_points_loop(ref_point, asp_dirs, mu)
+
+
+def _ref_dirs_from_points_loop(ref_point, asp_dirs, mu):
+    """The per-point loop of get_ref_dirs_from_points as pymoo writes it (any number of
+    aspiration directions); tests/test_oracle_survival_cpu.py pins the vectorised one-direction
+    path above to it."""
+    n_obj = ref_point.shape[1]
+    nvec = np.ones(n_obj) / np.sqrt(n_obj)
+    p0 = np.eye(n_obj)[0]
     val = []
     for point in ref_point:
         r = mu * np.array(asp_dirs, dtype=np.float64, copy=True)
@@ -622,6 +632,9 @@ def associate(F, ref_dirs, ideal, nadir):
     return niche, dist[np.arange(F.shape[0]), niche]
 
 
+NICHE_KEY_BLOCK = 8  # rounds of niche-order keys drawn per Philox batch in niching()
+
+
 def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
     """[pymoo-recall] nsga3.niching with Philox draws replacing np.random:
     * ``np.random.permutation(next_niches)[:n_select]`` in loop iteration ``round`` ->
@@ -644,8 +657,9 @@ def niching(n_remaining, niche_count, niche_of, dist, seed, gen, stream_key=0):
     # members of each niche in increasing position (np.where order)
     by_niche = np.argsort(niche_of, kind="stable")
     starts = np.searchsorted(niche_of[by_niche], np.arange(n_niches + 1))
-    # niche-order keys are drawn for blocks of rounds at once (same counters)
-    kblk, k0, KB = None, -1, 8
+    # niche-order keys are drawn for blocks of rounds at once (same counters; the block
+    # size changes nothing: tests/test_oracle_survival_cpu.py)
+    kblk, k0, KB = None, -1, NICHE_KEY_BLOCK
     while len(survivors) < n_remaining:
         n_select = n_remaining - len(survivors)
         nl = np.unique(niche_of[mask])

@@ -15,6 +15,7 @@ RES = os.path.join(PKG, "resources")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs via the C-ABI library)")
+    config.addinivalue_line("markers", "slow: CPU test of more than ~10 s (still in the default run)")
 
 
 @pytest.fixture(scope="session")

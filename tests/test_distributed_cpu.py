@@ -135,3 +135,91 @@ def test_bench_step_is_generate_sharded(B_all, world, shard):
         per = -(-n_glob // world)
         mine = max(0, min(n_glob, (rank + 1) * per) - rank * per)
         assert calls == ([mine] * 2 if mine else [])
+
+
+THR = {"f1": 0.5, "f2": 0.3}
+
+
+def fake_scored_objectives(x):
+    """Deterministic per-state final-population objectives (b, n=6, 3) and ML candidates
+    (b, 6, 5) with ties in f1, NaNs and states without an o7 success."""
+    xs = torch.as_tensor(np.asarray(x, np.float64))
+    b = xs.shape[0]
+    k = torch.arange(6, dtype=torch.float64)
+    s = xs.sum(1)[:, None]
+    cv = torch.remainder(s + k, 3.0) - 1.0          # <= 0 for two of three candidates
+    f1 = torch.remainder(0.37 * s + 0.11 * k, 1.0)
+    f1[:, 4] = f1[:, 1]                              # an f1 tie
+    f2 = torch.remainder(0.23 * s + 0.07 * k, 0.6)
+    f2[torch.arange(b) % 3 == 2, 5] = float("nan")   # NaN compares false
+    obj = torch.stack([cv, f1, f2], dim=-1)
+    xf = xs[:, None, :] + k[None, :, None]
+    return obj, xf
+
+
+def ref_success(obj, xf):
+    """numpy restatement of objective_calculator.py:86-101 (_objective_respected), :121-128
+    (any over the population) and :153-182 (_get_one_successful, misclassification asc,
+    max_inputs=1; stable order among equal f1)."""
+    flags, best = [], []
+    for o, x in zip(obj, xf):
+        c, m, l = o[:, 0] <= 0, o[:, 1] < THR["f1"], o[:, 2] <= THR["f2"]
+        r = np.column_stack([c, m, l, c * m, c * l, m * l, c * m * l])
+        flags.append(r.any(axis=0))
+        idx = np.argsort(o[:, 1], kind="stable")[r[:, -1][np.argsort(o[:, 1], kind="stable")]]
+        best.append(x[idx[0]] if idx.size else np.full(x.shape[1], np.nan))
+    return np.array(flags), np.array(best)
+
+
+def _scored_worker(rank, world, port, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from moeva2_amd.distributed import generate_scored_sharded, success_flags
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
+    calls = []
+
+    def attack(xs, mc):
+        if len(xs) == 0:
+            raise ValueError("bad mv_set_states arguments")
+        calls.append(len(xs))
+        obj, xf = fake_scored_objectives(xs)
+        return success_flags(obj, xf, THR)
+
+    flags, best = generate_scored_sharded(attack, x, 1, 5)
+    q.put((rank, calls, flags.numpy(), best.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B,world", [(7, 2), (1, 2), (5, 4), (2, 3), (9, 3)])
+def test_scored_sharded_gathers_flags(B, world):
+    """generate_scored_sharded: every rank scores its own slice and only per-state o1..o7
+    flags (uint8) and one successful candidate per state are gathered; every rank ends with
+    the unsharded verdict in state order, empty ranks included."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scored_worker, args=(r, world, port, B, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
+    obj, xf = fake_scored_objectives(x)
+    ref_f, ref_b = ref_success(obj.numpy(), xf.numpy())
+    assert ref_f[:, 6].any() and not ref_f[:, 6].all() or B < 3
+    per = -(-B // world)
+    for rank, calls, flags, best in res:
+        assert flags.dtype == np.uint8 and flags.shape == (B, 7)
+        np.testing.assert_array_equal(flags.astype(bool), ref_f)
+        np.testing.assert_array_equal(best, ref_b)
+        mine = max(0, min(B, (rank + 1) * per) - rank * per)
+        assert calls == ([mine] if mine else [])

@@ -681,6 +681,54 @@ def test_generate_sharded_real_engine_world1():
         dist.destroy_process_group()
 
 
+def test_generate_scored_sharded_real_engine_world1():
+    """Moeva2.generate_scored_sharded on a one-rank RCCL group: the gathered per-state o1..o7
+    flags equal the ObjectiveCalculator's verdict on an unsharded generate of the same states
+    (success_rate_3d, objective_calculator.py:121-128), the successful candidates are the
+    o7-successful rows with the smallest f1 (_get_one_successful, :153-182), and per-state
+    streams keyed by the global state index give the same populations unsharded."""
+    import socket
+
+    import torch.distributed as dist
+
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+
+    name = "botnet"
+    c = make_constraints(name)
+    p = Project(name)
+    sc = make_scaler(name)
+    m = Moeva2(os.path.join(RES, PROJECTS[name][1]), c, ml_scaler=sc, norm=2, n_gen=30,
+               n_pop=40, n_offsprings=20, seed=11, state_streams=True)
+    X = p.x[:6]
+    calc = ObjectiveCalculator(make_classifier(name), c, 1, {"f1": 0.5, "f2": 4.0},
+                               min_max_scaler=sc, ml_scaler=sc, norm=2)
+    res = m.generate(X, 1)
+    x_f = np.stack([m._encoder.genetic_to_ml(np.stack([ind.X for ind in r.pop]), X[b])
+                    for b, r in enumerate(res)])
+    obj = calc.calculate_objectives_3d(X, x_f)
+    resp = np.stack([calc._objective_respected(o) for o in obj])
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        flags, best = m.generate_scored_sharded(X, 1, calc)
+    finally:
+        dist.destroy_process_group()
+    np.testing.assert_array_equal(flags, resp.any(axis=1))
+    np.testing.assert_array_equal(flags.mean(axis=0), calc.success_rate_3d(X, x_f))
+    for b in range(X.shape[0]):
+        ok = resp[b][:, 6]
+        if ok.any():
+            f1 = np.where(ok, obj[b][:, 1], np.inf)
+            np.testing.assert_array_equal(best[b], x_f[b][int(np.argmin(f1))])
+        else:
+            assert np.isnan(best[b]).all()
+
+
 def test_success_rate_matches_oracle_attack():
     """End to end (north_star): the constrained success rates o1..o7
     (objective_calculator.py:86-119) of the device attack against the oracle's CPU attack

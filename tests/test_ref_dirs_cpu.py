@@ -65,13 +65,20 @@ def test_shipped_dirs_vs_riesz_energy_method(restated, n):
     assert _cover_radius(X, rng) <= 1.5 * _cover_radius(R, rng)
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("n", [200, 640])
 def test_shipped_dirs_are_the_generator_output(n):
-    """resources/ref_dirs/energy_3_{n}_seed1.npy == riesz_energy_dirs(3, n, seed=1)."""
+    """resources/ref_dirs/energy_3_{n}_seed1.npy is riesz_energy_dirs(3, n, seed=1): the same
+    points up to the rounding a different numpy / BLAS / SIMD dispatch may introduce over
+    ~1000 Adam steps (a tight tolerance, not bit equality), the same log-energy."""
     from moeva2_amd.attacks.moeva2 import ref_dirs as rd
 
     X = np.load(f"{rd._RES}/energy_3_{n}_seed1.npy", allow_pickle=False)
-    np.testing.assert_array_equal(X, rd.riesz_energy_dirs(3, n, seed=1))
+    Y = rd.riesz_energy_dirs(3, n, seed=1)
+    assert X.shape == Y.shape
+    np.testing.assert_allclose(X, Y, rtol=0, atol=1e-9)
+    e_x, e_y = rp.riesz_log_energy(X, 6.0), rp.riesz_log_energy(Y, 6.0)
+    assert abs(e_x - e_y) <= 1e-9 * abs(e_y)
 
 
 def test_generator_projection_and_energy_gradient():
