@@ -378,6 +378,39 @@ def test_survival_bit_exact_vs_oracle(N, n_survive):
             np.testing.assert_array_equal(state["extreme"][b].reshape(3, 3), ost[b].extreme)
 
 
+def test_survival_bit_exact_on_clone_heavy_botnet_states(golden):
+    """Survival inputs of real botnet attack generations where the merged population is
+    mostly clones (41-93 distinct objective rows of 303, one front of ~275 individuals, so
+    niching picks 203 of them): recorded from the device by tools/surv_dump.py when the
+    survivors were not distinct (round 4).  The survivors must be distinct and bit-exact vs
+    the oracle, with every intermediate (ranks, order, niches, distances, nadir)."""
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    d = golden("survival_botnet_clones.npz")
+    F = d["F"]
+    B, N, _ = F.shape
+    n_survive = int(d["n_survive"])
+    ref = energy_ref_dirs(3, int(d["n_pop"]), seed=1)
+    asp = np.full((1, 3), 1.0 / 3.0)
+    for b in range(B):
+        state = dict(ideal=d["ideal"][b:b + 1], worst=d["worst"][b:b + 1],
+                     extreme=d["extreme"][b:b + 1], has=d["has_extreme"][b:b + 1])
+        seed, gen = int(d["seed"][b]), int(d["gen"][b])
+        got = _run_survive(F[b:b + 1], ref, n_survive, seed, gen, state)
+        ost = mo.SurvivalState(ideal=d["ideal"][b].copy(), worst=d["worst"][b].copy(),
+                               extreme=d["extreme"][b].reshape(3, 3).copy()
+                               if d["has_extreme"][b] else None)
+        r = mo.survive(F[b], n_survive, ost, ref, asp, 0.05, seed, gen)
+        nr = len(np.concatenate(r.fronts))
+        assert got["nr"][0] == nr
+        np.testing.assert_array_equal(got["order"][0, :nr], np.concatenate(r.fronts))
+        np.testing.assert_array_equal(got["nadir"][0], r.nadir)
+        np.testing.assert_array_equal(got["niche"][0, :nr], r.niche)
+        np.testing.assert_array_equal(got["dist"][0, :nr], r.dist)
+        assert len(set(got["surv"][0].tolist())) == n_survive, f"state {b}: duplicate survivors"
+        np.testing.assert_array_equal(got["surv"][0], r.survivors)
+
+
 def _oracle_attack_merges(prob, ref, G, P, O, seed):
     """The merged objective arrays the oracle's attack hands to survival, per generation."""
     asp = np.full((1, 3), 1.0 / 3.0)
