@@ -1074,6 +1074,13 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       fill[n] = 0;
     }
     for (int l = tid; l < nlev; l += T) L.lround[l] = 0;
+    // The counters above must be zero before ANY thread counts into them.  (Round 3 had no
+    // barrier here: a thread of one wave could add its member to mcnt[n] / cnt[n] before the
+    // thread of another wave that zeroes entry n ran, and the zeroing store erased the count.
+    // With few crowded niches -- clone-heavy botnet generations: 2-7 niches for ~270
+    // last-front members -- the member lists then overlapped and niching returned duplicate
+    // survivors; found by the checks build, check 26, tests/golden/survival_botnet_clones.npz.)
+    __syncthreads();
     unsigned long long* sk = L.sortk;
     for (int p = tid; p < until; p += T) atomicAdd(&cnt[L.niche[p]], 1);
     // member order inside each niche: ascending (niche, member key, position); grank = rank
