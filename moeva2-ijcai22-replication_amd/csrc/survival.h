@@ -283,93 +283,6 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
   }
 }
 
-// Packed-rank dominance.  r_k(i) = #{j : F_k(j) < F_k(i)} preserves <, = and > between the
-// values of objective k (no NaN), so i dominates j (all F_k(i) <= F_k(j), one <) exactly
-// when all r_k(i) <= r_k(j) and the rank triples differ.  The three ranks pack into one
-// word, FB bits per field, the top bit of each field a guard: (P(j) | G) - P(i) keeps guard
-// k set iff r_k(j) >= r_k(i) (a field never borrows from the next: r < 2^(FB-1)), so
-// "all <=" is one subtract, one AND and one compare -- instead of six fp64 compares and
-// their masks per direction.  FB = 10 (u32) for N <= 512, 11 (u64) for N <= 1024.
-template <class W, int FB>
-__device__ __forceinline__ W rank_guards() {
-  return ((W)1 << (FB - 1)) | ((W)1 << (2 * FB - 1)) | ((W)1 << (3 * FB - 1));
-}
-
-// Ranks of the N individuals in the three objectives (counts of strictly smaller values,
-// one (objective, individual) item per thread), then the packed words in L.dist.  Ends on
-// a barrier.  The rank temporaries use L.key / L.surv / L.csr (free until the NDS).
-template <class W, int FB, int T>
-__device__ __forceinline__ void packed_ranks(SurvLds& L, const int N) {
-  const int tid = threadIdx.x;
-  int* rk[3] = {L.key, L.surv, L.csr};
-  for (int t = tid; t < 3 * N; t += T) {
-    const int k = t >= 2 * N ? 2 : (t >= N ? 1 : 0);
-    const int i = t - k * N;
-    const double* f = L.F + k;
-    const double v = f[i * 3];
-    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    int j = 0;
-    for (; j + 4 <= N; j += 4) {
-      c0 += f[j * 3] < v ? 1 : 0;
-      c1 += f[j * 3 + 3] < v ? 1 : 0;
-      c2 += f[j * 3 + 6] < v ? 1 : 0;
-      c3 += f[j * 3 + 9] < v ? 1 : 0;
-    }
-    for (; j < N; ++j) c0 += f[j * 3] < v ? 1 : 0;
-    rk[k == 0 ? 0 : (k == 1 ? 1 : 2)][i] = (c0 + c1) + (c2 + c3);
-  }
-  __syncthreads();
-  W* P = (W*)L.dist;
-  for (int i = tid; i < N; i += T)
-    P[i] = (W)L.key[i] | ((W)L.surv[i] << FB) | ((W)L.csr[i] << (2 * FB));
-  __syncthreads();
-}
-
-// The dominance work items of the six-compare pass (unordered 64 x 64 block pairs x four
-// 16-row quarters, from the LDS counter iscal[14]) on the packed words: the same bits.
-template <class W, int FB>
-__device__ __forceinline__ void dominance_items_packed(SurvLds& L, const int N, const int NW,
-                                                       const int lane) {
-  unsigned short* dom16 = (unsigned short*)L.dom;
-  const W* P = (const W*)L.dist;
-  const W G = rank_guards<W, FB>();
-  const int n_q = NW * (NW + 1) * 2;
-  for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
-    t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
-    if (t >= n_q) break;
-    const int qq = t & 3;
-    int qi = 0, rem = t >> 2;
-    while (rem >= NW - qi) {
-      rem -= NW - qi;
-      ++qi;
-    }
-    const int qj = qi + rem;
-    const int i = qi * 64 + lane;
-    const bool vi = i < N;
-    const W Pi = P[vi ? i : 0];
-    const W PiG = Pi | G;
-    const int j0 = qj * 64 + qq * 16;
-    unsigned long long mine = 0ull;
-    unsigned acc = 0u;
-#pragma unroll 4
-    for (int u = 0; u < 16; ++u) {
-      const int j = j0 + u;
-      const bool vj = j < N;
-      const W Pj = P[vj ? j : 0];
-      const bool ne = Pi != Pj;
-      const bool le_ij = (((Pj | G) - Pi) & G) == G;  // every r_k(i) <= r_k(j)
-      const bool le_ji = ((PiG - Pj) & G) == G;
-      const unsigned long long m = __ballot(vi && vj && ne && le_ij);
-      mine = lane == u ? m : mine;
-      acc |= (vi && vj && ne && le_ji) ? (1u << u) : 0u;
-    }
-    if (lane < 16 && j0 + lane < N) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
-    if (qi != qj && i < N) dom16[((size_t)i * NW + qj) * 4 + qq] = (unsigned short)acc;
-  }
-}
-
 // NWMAX: dominance words per individual held in registers (N <= 64 NWMAX); above
 // SURV_NLDS the bitsets go to the HBM scratch a.dom_g instead of LDS.
 // a: pointers and sizes (slot or dense mode); b: the state; N, gen, sel_gen and
@@ -436,8 +349,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   PHASE(0)
 
   // ---- load merged F, ref points
-  static_assert(T / 64 <= 13, "per-wave NaN flags live in iscal[0, 13)");
-  bool any_nan = false;
   for (int m = tid; m < N; m += T) {
     int s = m;
     const double* src;
@@ -448,17 +359,13 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     } else {
       src = a.F + ((size_t)b * N + m) * 3;
     }
-    const double f0 = src[0], f1 = src[1], f2 = src[2];
-    L.F[m * 3 + 0] = f0;
-    L.F[m * 3 + 1] = f1;
-    L.F[m * 3 + 2] = f2;
-    any_nan |= (f0 != f0) | (f1 != f1) | (f2 != f2);
+    L.F[m * 3 + 0] = src[0];
+    L.F[m * 3 + 1] = src[1];
+    L.F[m * 3 + 2] = src[2];
     L.slot[m] = s;
     L.front_of[m] = -1;
     L.sel[m] = 0;
   }
-  // per-wave NaN flags (iscal[0, T/64)): the packed-rank dominance needs a total order
-  if (lane == 0) L.iscal[wave] = __ballot(any_nan) != 0ull;
   for (int m = N + tid; m < NW * 64; m += T) {  // padding rows: compare false both ways
     L.F[m * 3 + 0] = __builtin_nan("");
     L.F[m * 3 + 1] = __builtin_nan("");
@@ -473,19 +380,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   }
   __syncthreads();
   PHASE(1)
-
-  // ---- per-objective ranks packed into one word per individual (no NaN objective: the
-  // ranks then preserve every <, = and > between objective values, so they decide
-  // dominance exactly); the words live in L.dist (free until the association)
-  bool nan_rows = false;
-  for (int w = 0; w < T / 64; ++w) nan_rows |= L.iscal[w] != 0;
-  const bool packed = !nan_rows;
-  if (packed) {
-    if (N <= 512)
-      packed_ranks<uint32_t, 10, T>(L, N);
-    else
-      packed_ranks<unsigned long long, 11, T>(L, N);
-  }
 
   // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: wave
   // 0, before it joins the dominance pass below (independent of it; its results are first
@@ -545,12 +439,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   // ballot is word qi of dom[j], kept by lane u); gt && !lt -> j dominates
   // i, bit u of this lane's 16-bit quarter qq of word qj of dom[i] (off-diagonal pairs
   // only: the diagonal block is covered by its ballots).
-  if (packed) {
-    if (N <= 512)
-      dominance_items_packed<uint32_t, 10>(L, N, NW, lane);
-    else
-      dominance_items_packed<unsigned long long, 11>(L, N, NW, lane);
-  } else {  // a NaN objective: the six-compare pass (NaN compares false both ways)
+  {
     unsigned short* dom16 = (unsigned short*)L.dom;
     const int n_q = NW * (NW + 1) * 2;  // block pairs x 4 quarters
     for (;;) {
