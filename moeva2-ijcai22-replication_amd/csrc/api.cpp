@@ -351,6 +351,31 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
       geo[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
     }
     put(vo.geo, geo.data(), (size_t)(V + 1) * 4);
+    {  // region S: k_genc's slim program (kernels.h); the packed words mirror rowops pack_op
+      const int n_lane = C - n_sd;
+      p.slim = n_lane <= 64 * OPS_REG;
+      std::vector<double> k1(C);
+      std::vector<int> sd((size_t)(n_sd > 0 ? n_sd : 1) * 4, 0);
+      std::vector<unsigned> opw(C);
+      for (int k = 0; k < C; ++k) {
+        k1[k] = sk[(size_t)k * 2];
+        const int* ar = &sarg[(size_t)k * 4];
+        if (k < n_lane) {
+          p.slim &= (scode[k] == MV_OP_DIFF || scode[k] == MV_OP_RATIO_SAFE) && ar[0] >= 0 &&
+                    ar[0] < 0x4000 && ar[1] >= 0 && ar[1] < 0x4000;
+          opw[k] = (unsigned)scode[k] | ((unsigned)ar[0] << 4) | ((unsigned)ar[1] << 18);
+        } else {
+          opw[k] = 0u;
+          for (int q = 0; q < 4; ++q) sd[(size_t)(k - n_lane) * 4 + q] = ar[q];
+        }
+      }
+      put(vo.s_k, k1.data(), (size_t)C * 8);
+      put(vo.s_col, scol.data(), (size_t)C * 4);
+      put(vo.s_pool, pd->idx_pool, (size_t)pd->n_pool * 4);
+      put(vo.s_sd, sd.data(), sd.size() * 4);
+      put(vo.s_opw, opw.data(), (size_t)C * 4);
+      if (std::getenv("MV_SLIM") && std::getenv("MV_SLIM")[0] == '0') p.slim = 0;  // A/B
+    }
     K((unsigned char**)&p.vblob, blob.data(), blob.size());
   }
   p.tol = pd->tol;

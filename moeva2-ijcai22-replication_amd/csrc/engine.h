@@ -101,6 +101,10 @@ struct DProblem {
   // is mutable feature g), so k_gen writes no fp32 ML row: the xml hand-off (Dm4 * 4 B
   // written + read back per row) is gone
   int xml_direct;
+  // every lane op of the constraint program is DIFF or RATIO_SAFE, at most OPS_REG per lane
+  // (rowops.h), plus ABS_SUMDIFF ops: k_genc's phase 2 stages the slim region S of the
+  // problem blob instead of region A (7-10 KiB less LDS per workgroup)
+  int slim;
 };
 
 struct DStates {

@@ -48,6 +48,11 @@ ArgRing g_rings[MAX_DEVICES];
 std::mutex g_ring_mu;
 }  // namespace
 
+size_t lds_pad(const char* env) {
+  const char* v = std::getenv(env);
+  return v ? (size_t)std::atol(v) : 0;
+}
+
 hipError_t stage_rows(const RowsArgs& a, hipStream_t stream, int* slot) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -220,7 +225,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   }
   glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
   if (ev && !REGC) {
-    glds_copy(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
+    glds_copy(smem + L.c_at, p.vblob + o.c_at, o.c_end - o.c_at, wave, lane);
     glds_copy(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
   }
   if (ev && !IDENT) glds_copy(smem + L.x_at, sblob, o.x_end, wave, lane);
@@ -442,7 +447,9 @@ __global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0
 // state x a chunk of its rows, as k_gen; the row's genes (written by k_gen) are scattered
 // into the wave's ML row buffer whose immutable features were written once, then each lane
 // evaluates its (register-packed) ops.
-template <bool FULL, bool IDENT, int NT>
+// SLIM (k_genc, DProblem.slim): region S staged instead of region A, the lane ops' packed
+// words loaded straight from the problem blob (see kernels.h).
+template <bool FULL, bool IDENT, int NT, bool SLIM = false>
 __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int rows_wg,
                                           unsigned char* smem, bool have_dst = false,
                                           int dst_pre = 0) {
@@ -479,8 +486,24 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   double xa[NT], xb[NT];
   if (nrw > 0) load_row(0, xa);
   if (nrw > 1) load_row(1, xb);
-  glds_copy<CONS_T>(smem, p.vblob, o.a_end, wave, lane);
-  glds_copy<CONS_T>(smem + o.a_end, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
+  // LDS: [program region (A, or S when SLIM)][X: x_init][one row buffer per wave]
+  const unsigned pa = SLIM ? o.s_end - o.s_at : o.a_end;
+  const int n_lane = p.C - p.n_sumdiff;
+  const int kops = min(OPS_REG, (n_lane + 63) >> 6);
+  unsigned opw[OPS_REG];
+  if (SLIM) {  // the packed words from HBM / L2, in flight across the staging
+    const unsigned* gw = (const unsigned*)(p.vblob + o.s_opw);
+#pragma unroll
+    for (int k = 0; k < OPS_REG; ++k) {
+      const int c = lane + 64 * k;
+      const unsigned w = gw[c < n_lane ? c : 0];
+      opw[k] = (k < kops && c < n_lane) ? w : 0u;
+    }
+    glds_copy<CONS_T>(smem, p.vblob + o.s_at, pa, wave, lane);
+  } else {
+    glds_copy<CONS_T>(smem, p.vblob, pa, wave, lane);
+  }
+  glds_copy<CONS_T>(smem + pa, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
   int ginf[NT];
   {
     const int* gi = (const int*)(p.vblob + o.ginfo);
@@ -494,30 +517,40 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
-  double* xrow = (double*)(smem + o.a_end + o.x_end + wave * o.rb);
+  double* xrow = (double*)(smem + pa + o.x_end + wave * o.rb);
   {
-    const double* s_xi = (const double*)(smem + o.a_end + o.xi);
+    const double* s_xi = (const double*)(smem + pa + o.xi);
     for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
   }
   OpTab tab;
-  tab.code = (const int*)(smem + o.opc);
-  tab.arg = (const int4*)(smem + o.opa);
-  tab.k = (const double2*)(smem + o.opk);
-  tab.col = (const int*)(smem + o.ocol);
-  tab.pool = (const int*)(smem + o.pool);
+  if (SLIM) {
+    tab.code = nullptr;
+    tab.arg = nullptr;
+    tab.k = nullptr;
+    tab.k1 = (const double*)(smem + (o.s_k - o.s_at));
+    tab.sd = (const int4*)(smem + (o.s_sd - o.s_at));
+    tab.col = (const int*)(smem + (o.s_col - o.s_at));
+    tab.pool = (const int*)(smem + (o.s_pool - o.s_at));
+  } else {
+    tab.code = (const int*)(smem + o.opc);
+    tab.arg = (const int4*)(smem + o.opa);
+    tab.k = (const double2*)(smem + o.opk);
+    tab.col = (const int*)(smem + o.ocol);
+    tab.pool = (const int*)(smem + o.pool);
+  }
   tab.C = p.C;
-  tab.n_lane = p.C - p.n_sumdiff;
+  tab.n_lane = n_lane;
   tab.tol = p.tol;
   if (a.hist) {
     tab.hlo = a.hist + (size_t)b * a.hist_rows * a.hist_w;
     tab.hhi = tab.hlo + (size_t)a.hist_rows * a.hist_w;
   }
-  unsigned opw[OPS_REG];
-  const int kops = min(OPS_REG, (tab.n_lane + 63) >> 6);
+  if (!SLIM) {
 #pragma unroll
-  for (int k = 0; k < OPS_REG; ++k) {
-    const int c = lane + 64 * k;
-    opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
+    for (int k = 0; k < OPS_REG; ++k) {
+      const int c = lane + 64 * k;
+      opw[k] = (k < kops && c < tab.n_lane) ? pack_op(tab, c) : 0u;
+    }
   }
   auto do_row = [&](int k, const double* x) {
     const int i = MV_IDX(rc.i0 + wave + CONS_W * k, a.n, CK_CONS_DST);
@@ -535,7 +568,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows +
                                       MV_IDX(hist_row0 + i, a.hist_rows, CK_CONS_DST)) * a.hist_w
                           : nullptr;
-    const double f3 = constraints_regs<FULL>(tab, opw, kops, xrow, lane, grow,
+    const double f3 = constraints_regs<FULL, SLIM>(tab, opw, kops, xrow, lane, grow,
                                              (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
     // The row's destination is read from lane k HERE, with every lane active: a readlane
     // of a lane that is inactive at that point returns an undefined value.  (Round 3 read
@@ -576,14 +609,18 @@ __global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int ro
 // the chain loses a launch boundary; the phases run one after the other, so the kernel
 // needs the larger of the two register and LDS footprints, not their sum (the fused row
 // loop of round 2, k_rows, kept both phases' registers live: 208 VGPRs).
-// MV_GENC_WAVES (development builds): k_genc's minimum waves per SIMD for the register
-// allocator (4: 128 VGPRs; the default, none, lets it use 148 and runs 3 per SIMD)
-#ifdef MV_GENC_WAVES
-#define MV_GENC_BOUNDS __launch_bounds__(VARY_T, MV_GENC_WAVES)
-#else
-#define MV_GENC_BOUNDS __launch_bounds__(VARY_T)
+// k_genc's minimum waves per SIMD for the register allocator: 4 (128 VGPRs; the two-point
+// instances up to 8 genes per lane spill a few registers to scratch) for a 4th resident
+// workgroup per CU -- with the slim phase-2 LDS (~37 KiB) four fit.  Round 4 A/B on the
+// botnet headline: 172.2 vs 161.5 M evals/s (k_genc 119.5 vs 137.6 us, one state group).
+// The SBX and 16-genes-per-lane instances keep the allocator's choice (their register needs
+// would spill heavily).  MV_GENC_WAVES (development builds) overrides the 4.
+#ifndef MV_GENC_WAVES
+#define MV_GENC_WAVES 4
 #endif
-template <bool IDENT, int NT, bool SBX>
+#define MV_GENC_BOUNDS \
+  __launch_bounds__(VARY_T, (NT <= 8 && !SBX) ? MV_GENC_WAVES : 1)
+template <bool IDENT, int NT, bool SBX, bool SLIM>
 __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -599,7 +636,7 @@ __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows
   // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  cons_rows<false, IDENT, NT>(a, hist_row0, rows_wg, smem, true, orow_v);
+  cons_rows<false, IDENT, NT, SLIM>(a, hist_row0, rows_wg, smem, true, orow_v);
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 7] = wall_clock64();
@@ -1800,17 +1837,29 @@ static bool use_genc(const RowsArgs& a) {
 
 template <int NT>
 static hipError_t genc_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen, int h0, int rw,
-                          bool sbx) {
+                          bool sbx, bool slim) {
   static bool configured = false;
   if (!configured) {
-    allow_lds(k_genc<true, NT, false>);
-    allow_lds(k_genc<true, NT, true>);
+    allow_lds(k_genc<true, NT, false, false>);
+    allow_lds(k_genc<true, NT, true, false>);
+    allow_lds(k_genc<true, NT, false, true>);
+    allow_lds(k_genc<true, NT, true, true>);
     configured = true;
   }
-  if (sbx)
-    hipLaunchKernelGGL((k_genc<true, NT, true>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
-  else
-    hipLaunchKernelGGL((k_genc<true, NT, false>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+#define GENC(X, Y) \
+  hipLaunchKernelGGL((k_genc<true, NT, X, Y>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw)
+  if (sbx) {
+    if (slim)
+      GENC(true, true);
+    else
+      GENC(true, false);
+  } else {
+    if (slim)
+      GENC(false, true);
+    else
+      GENC(false, false);
+  }
+#undef GENC
   return hipGetLastError();
 }
 
@@ -1832,14 +1881,16 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const bool sbx = a.mode == 1 && a.cx_kind == 1;
     const GenLds gl = gen_lds(o, gen_regc(a.p, nt), true, true);
     const size_t lg = sbx ? gen_lds_sbx(gl, nt) : gl.total;
-    const size_t lc = cons_lds_total(o);
-    const size_t lds = lg > lc ? lg : lc;
-    if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
-    if (nt == 5) return genc_go<5>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
-    if (nt == 6) return genc_go<6>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
-    if (nt == 7) return genc_go<7>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
-    if (nt == 8) return genc_go<8>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
-    return genc_go<16>(grid, lds, stream, slot, gen, hist_row0, rw, sbx);
+    const bool slim = a.p.slim != 0;
+    const size_t lc = slim ? cons_lds_slim(o) : cons_lds_total(o);
+    static const size_t pad = lds_pad("MV_LDS_PAD_GENC");
+    const size_t lds = (lg > lc ? lg : lc) + pad;
+    if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
+    if (nt == 5) return genc_go<5>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
+    if (nt == 6) return genc_go<6>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
+    if (nt == 7) return genc_go<7>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
+    if (nt == 8) return genc_go<8>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
+    return genc_go<16>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
   }
   const int B = a.total / a.n;
   const int rw = vary_rows_per_wg(a.n);
@@ -1926,7 +1977,8 @@ static hipError_t mlp2_go3(const RowsArgs& a, int slot, int hist_row0, hipStream
     allow_lds(k_mlp2<CJ, BF, DIRECT, CO>);
     configured = true;
   }
-  const size_t lds = mlp2_lds(a.p);
+  static const size_t pad = lds_pad("MV_LDS_PAD_MLP");
+  const size_t lds = mlp2_lds(a.p) + pad;
   if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlp2<CJ, BF, DIRECT, CO>, 256, lds) != hipSuccess ||

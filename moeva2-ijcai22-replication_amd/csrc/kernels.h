@@ -29,12 +29,17 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
 //                 B: mutation gap table, gene table, mutable features,
 //                    one-hot group offsets / features                     -> k_gen
 //                 C: ML scaler at the mutable features (mlS, mlM)         -> k_gen
+//                 S: the slim program of k_genc's phase 2 (DIFF / RATIO_SAFE lane ops and
+//                    ABS_SUMDIFF only): k (fp64), col, pool, sum-diff args -> LDS; the
+//                    ops' packed words (code | a0 << 4 | a1 << 18) read from HBM
 //   state blob    X: x_init                                               -> k_cons (k_gen OHE)
 //                 E: encoder MinMax at the mutable features (es, em, x0)  -> k_gen
 struct VaryOff {
   unsigned opa, opk, opc, ocol, pool, a_end;      // region A at 0
   unsigned geo, ginfo, mutf, ooff, ofeat, b_at, b_end;  // region B at b_at
-  unsigned mlS, mlM, c_at, vb;                    // region C at c_at; vb = blob bytes
+  unsigned mlS, mlM, c_at, c_end;                 // region C at c_at
+  unsigned s_k, s_col, s_pool, s_sd, s_at, s_end;  // region S (staged part) at s_at
+  unsigned s_opw, vb;                             // S packed op words; vb = blob bytes
   unsigned xi, x_end;                             // region X at 0
   unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
   unsigned rb;                                    // ML row buffer bytes
@@ -67,6 +72,16 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   off = o.c_at;
   o.mlS = take(Dm4 * 8);
   o.mlM = take(Dm4 * 8);
+  o.c_end = kb(off);
+  o.s_at = o.c_end;
+  off = o.s_at;
+  o.s_k = take(C * 8);
+  o.s_col = take(C * 4);
+  o.s_pool = take((size_t)p.n_pool * 4);
+  o.s_sd = take((size_t)(p.n_sumdiff > 0 ? p.n_sumdiff : 1) * 16);
+  o.s_end = kb(off);
+  off = o.s_end;
+  o.s_opw = take(C * 4);
   o.vb = kb(off);
   off = 0;
   o.xi = take((size_t)p.D * 8);
@@ -97,7 +112,7 @@ __host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool iden
   at += o.b_end - o.b_at;
   if (eval && !regc) {
     l.c_at = at;
-    at += o.vb - o.c_at;
+    at += o.c_end - o.c_at;
     l.e_at = at;
     at += o.sb - o.e_at;
   }
@@ -121,6 +136,10 @@ __host__ __device__ inline unsigned gen_lds_sbx(const GenLds& l, int nt) {
 __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + CONS_W * o.rb;
 }
+// k_genc's phase 2 with the slim program (DProblem.slim): region S, region X, one row per wave
+__host__ __device__ inline unsigned cons_lds_slim(const VaryOff& o) {
+  return (o.s_end - o.s_at) + o.x_end + CONS_W * o.rb;
+}
 
 // k_predict: TR-row tiles (32, or 16 for inputs too wide for a 32-row tile)
 __host__ __device__ inline size_t predict_region1_bytes(int D4, int hmax, int TR) {
@@ -133,6 +152,11 @@ __host__ __device__ inline size_t predict_lds_bytes(int D4, int hmax, int Klast,
   return mlp_head_bytes(Klast, nout) + predict_region1_bytes(D4, hmax, TR) +
          (size_t)TR * (hmax + 1) * sizeof(float);
 }
+
+// Development sensitivity knob: MV_LDS_PAD_<KERNEL> extra bytes of dynamic LDS requested
+// by a launch (GENC, MLP, SURV), to measure how the chain's throughput depends on each
+// kernel's LDS footprint (co-residency on a CU).  0 when unset.
+size_t lds_pad(const char* env);
 
 hipError_t launch_predict(const MlpArgs& a, hipStream_t stream);
 hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, const double* genes,

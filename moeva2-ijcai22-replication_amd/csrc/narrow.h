@@ -37,7 +37,7 @@ __host__ __device__ inline NarrowLds narrow_lds(const VaryOff& o, const DProblem
   l.b_at = at;
   at += o.b_end - o.b_at;
   l.c_at = at;
-  at += o.vb - o.c_at;
+  at += o.c_end - o.c_at;
   l.m_at = at;
   at += ((unsigned)p.D * 4 + 15) & ~15u;
   l.rows_at = at;
@@ -111,7 +111,7 @@ __device__ __forceinline__ void narrow_rows(const RowsArgs& a, int gen, int hist
   const NarrowLds L = narrow_lds(o, p);
   glds_copy<NARROW_T>(smem + L.a_at, p.vblob, o.a_end, wave, lane);
   glds_copy<NARROW_T>(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
-  glds_copy<NARROW_T>(smem + L.c_at, p.vblob + o.c_at, o.vb - o.c_at, wave, lane);
+  glds_copy<NARROW_T>(smem + L.c_at, p.vblob + o.c_at, o.c_end - o.c_at, wave, lane);
   int* mslot = (int*)(smem + L.m_at);
   for (int f = tid; f < p.D; f += NARROW_T) mslot[f] = -1;
   __builtin_amdgcn_s_waitcnt(0);

@@ -39,6 +39,9 @@ struct OpTab {
   double tol;
   const double* hlo = nullptr;  // checks builds: the state's history / G range [hlo, hhi)
   const double* hhi = nullptr;
+  // slim program (k_genc phase 2, region S): k as fp64 [C], the ABS_SUMDIFF args [C - n_lane]
+  const double* k1 = nullptr;
+  const int4* sd = nullptr;
 };
 
 __device__ __forceinline__ OpTab global_tab(const DProblem& p) {
@@ -116,7 +119,7 @@ __device__ __forceinline__ double eval_op(const OpTab& t, int c, const XR& x) {
 // differences (exact for the integer-valued features of every shipped program; the
 // summation order differs from numpy otherwise).
 __device__ __forceinline__ double sumdiff_wave(const OpTab& t, int c, const double* x, int lane) {
-  const int4 ar = t.arg[c];
+  const int4 ar = t.sd ? t.sd[c - t.n_lane] : t.arg[c];
   double s = 0.0;
   for (int q = ar.x + lane; q < ar.y; q += 64) s += x[t.pool[q]];
   for (int q = ar.y + lane; q < ar.z; q += 64) s -= x[t.pool[q]];
@@ -162,7 +165,8 @@ __device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
   return (unsigned)t.code[c] | ((unsigned)ar.x << 4) | ((unsigned)ar.y << 18);
 }
 
-template <bool FULL>
+// SLIM: every lane op is DIFF / RATIO_SAFE and held in opw (DProblem.slim); k from t.k1.
+template <bool FULL, bool SLIM = false>
 __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigned* opw, int kops,
                                                    const double* xrow, int lane, double* grow,
                                                    double* hcols) {
@@ -184,9 +188,9 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
       if (code == 1)
         v = va[k] - vb[k];
       else if (code == 2)
-        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k[c].x;
+        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - (SLIM ? t.k1[c] : t.k[c].x);
       else
-        v = eval_op<FULL>(t, c, xrow);
+        v = SLIM ? __builtin_nan("") : eval_op<FULL>(t, c, xrow);
       if (v <= t.tol) v = 0.0;
       const double g = v * (v > 0.0 ? 1.0 : 0.0);
       const int col = MV_IDX(t.col[c], t.C, CK_CONS_COL);
@@ -195,7 +199,7 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
       acc3 += g;
     }
   }
-  for (int c = lane + 64 * OPS_REG; c < t.n_lane; c += 64) {
+  for (int c = lane + 64 * OPS_REG; !SLIM && c < t.n_lane; c += 64) {
     double v = eval_op<FULL>(t, c, xrow);
     if (v <= t.tol) v = 0.0;
     const double g = v * (v > 0.0 ? 1.0 : 0.0);

@@ -611,6 +611,25 @@ def test_narrow_rows_match_wave_kernels(monkeypatch, name, B, P, O, G, hist, nor
     np.testing.assert_array_equal(h1.cpu().numpy(), h0.cpu().numpy())
 
 
+@pytest.mark.parametrize("name,B,P,O,G,hist,cx", [
+    ("botnet", 9, 203, 100, 5, 2, "two_point"), ("botnet", 5, 43, 20, 6, 1, "sbx"),
+    ("botnet", 4, 643, 320, 3, 0, "two_point")])
+def test_slim_program_matches_full(monkeypatch, name, B, P, O, G, hist, cx):
+    """k_genc's phase 2 with the slim program region (DIFF / RATIO_SAFE / ABS_SUMDIFF ops:
+    region S of the problem blob, the op words from HBM) is bit-identical to the full
+    region A: genes, F and the full history with every G column."""
+    X = Project(name).x[:B]
+    monkeypatch.setenv("MV_SLIM", "1")
+    e1, g1, F1, h1, _ = _attack(name, X, G, 29, hist=hist, P=P, O=O, mode="chain", crossover=cx)
+    assert e1.prog.C > 0
+    monkeypatch.setenv("MV_SLIM", "0")
+    _, g0, F0, h0, _ = _attack(name, X, G, 29, hist=hist, P=P, O=O, mode="chain", crossover=cx)
+    np.testing.assert_array_equal(g1.cpu().numpy(), g0.cpu().numpy())
+    np.testing.assert_array_equal(F1.cpu().numpy(), F0.cpu().numpy())
+    if hist:
+        np.testing.assert_array_equal(h1.cpu().numpy(), h0.cpu().numpy())
+
+
 def test_attack_invariants_lcld():
     """Whole device loop: bounds, integrality, F == re-evaluation, history layout.  (Each
     generation's kernels are pinned bit-exactly above; the loop is compared end to end
