@@ -618,8 +618,11 @@ __global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int ro
 #ifndef MV_GENC_WAVES
 #define MV_GENC_WAVES 4
 #endif
+#ifndef MV_GENC_SBX_WAVES
+#define MV_GENC_SBX_WAVES 1
+#endif
 #define MV_GENC_BOUNDS \
-  __launch_bounds__(VARY_T, (NT <= 8 && !SBX) ? MV_GENC_WAVES : 1)
+  __launch_bounds__(VARY_T, NT > 8 ? 1 : (SBX ? MV_GENC_SBX_WAVES : MV_GENC_WAVES))
 template <bool IDENT, int NT, bool SBX, bool SLIM>
 __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");
