@@ -35,7 +35,7 @@ constexpr int SURV_TMAX = 1024;  // largest survival workgroup (reduction scratc
 
 struct SurvLds {
   double* F;        // [N*3]
-  double* ref;      // [R*3]
+  const double* ref;  // global: the reference points (read-only, L2-resident)      // [R*3]
   double* U;        // [(R+3)*3] normalised reference directions
   float4* Uf;       // [R+3] the same in fp32 (association pre-filter)
   double* dist;     // [N]
@@ -82,6 +82,11 @@ struct SurvOff {
       dmin, lround, total;
 };
 
+// Niching's temporaries (count, remain, csr_off, csr, cand, ckey, dmin, lround) are dead
+// before the NDS ends and the dominance bitsets after it, so when the bitsets live in LDS
+// (N <= SURV_NLDS) and the temporaries fit inside them they share those bytes; the
+// reference points are read from global memory (L2-resident, the same for every state).
+// Round 4: 68.8 -> ~53 KiB per workgroup at N = 303, R = 200 (three workgroups per CU).
 __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
   const bool dom_lds = N <= SURV_NLDS;
   const unsigned NW = (N + 63) / 64;
@@ -92,11 +97,11 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   o.field = off;                  \
   off = (unsigned)align16(off + (size_t)(bytes));
   TAKE(F, (size_t)NW * 64 * 3 * 8)  // rows past N hold NaN (dominance padding)
-  TAKE(ref, (size_t)R * 3 * 8)
+  o.ref = 0;                        // unused: a.ref in global memory
   TAKE(U, (size_t)RN * 3 * 8)
   TAKE(Uf, (size_t)RN * 16)
   TAKE(dist, (size_t)N * 8)
-  TAKE(red, (SURV_TMAX / 64) * 16 * 8)
+  TAKE(red, (SURV_T / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
   TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)
@@ -111,19 +116,30 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(surv, N * 4)
   TAKE(sel, N * 4)
   TAKE(fstart, (N + 2) * 4)
+  TAKE(iscal, (16 + SURV_TMAX / 64) * 4)
+  TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
+  TAKE(perm, (size_t)Pperm * 4)
+  const unsigned end = off;
+  // the niching temporaries: inside the dominance bitsets when they fit, else appended
+  auto tsize = [&]() {
+    unsigned t = 0;
+    for (size_t b : {(size_t)RN * 4, (size_t)RN * 4, (size_t)(RN + 1) * 4, (size_t)N * 4,
+                     (size_t)RN * 4, (size_t)RN * 4, (size_t)RN * 8, (size_t)(2 * N + 2) * 4})
+      t = (unsigned)align16(t + b);
+    return t;
+  };
+  const bool alias = dom_lds && tsize() <= (unsigned)((size_t)N * NW * 8);
+  off = alias ? o.dom : end;
   TAKE(count, RN * 4)
   TAKE(remain, RN * 4)
   TAKE(csr_off, (RN + 1) * 4)
   TAKE(csr, N * 4)
   TAKE(cand, RN * 4)
   TAKE(ckey, RN * 4)
-  TAKE(iscal, (16 + SURV_TMAX / 64) * 4)
-  TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
-  TAKE(perm, (size_t)Pperm * 4)
   TAKE(dmin, (size_t)RN * 8)
   TAKE(lround, (size_t)(2 * N + 2) * 4)
 #undef TAKE
-  o.total = off;
+  o.total = alias ? end : off;
   return o;
 }
 
@@ -299,7 +315,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   const SurvOff o = surv_offsets(N, R, pslots);
   SurvLds L;
   L.F = (double*)(smem + o.F);
-  L.ref = (double*)(smem + o.ref);
+  L.ref = a.ref;  // global (surv_offsets)
   L.U = (double*)(smem + o.U);
   L.Uf = (float4*)(smem + o.Uf);
   L.dist = (double*)(smem + o.dist);
@@ -371,7 +387,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     L.F[m * 3 + 1] = __builtin_nan("");
     L.F[m * 3 + 2] = __builtin_nan("");
   }
-  for (int r = tid; r < R * 3; r += T) L.ref[r] = a.ref[r];
   if (tid < 9) pext[tid] = a.extreme[(size_t)b * 9 + tid];
   if (tid == 0) L.iscal[14] = 0;  // dominance work counter
   for (int q = tid; q < NW; q += T) {
