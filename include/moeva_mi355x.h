@@ -231,6 +231,18 @@ int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
 /* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
 int mv_attack_history(mv_engine* e, double* hist, void* stream);
+/* The attack's gene layout for the bound states (engine extension; no reference
+ * counterpart).  mv_set_states finds the genes no attack on those states can change --
+ * integer genes whose bounds are equal and whose initial value is that bound in every state
+ * (crossover swaps equal values, mutation clamps back to the bound; botnet: 120 of 432) --
+ * and the attack neither stores, moves nor sums them: their features are evaluated as
+ * immutable features (decoded from x_init, folded into the layer-1 bias, absent from f2's
+ * sum).  Every draw stays defined over all V genes, so the populations are those of the
+ * full layout; f1 / f2 follow the engine's summation order over the stored genes
+ * (oracle/device_order.py, `fixed`).  mv_evaluate / mv_decode / mv_variation always use
+ * every gene.  stored (may be NULL) [V] receives 1 for a stored gene, 0 for a fixed one;
+ * *n_stored the stored count (= V when nothing is fixed, or MV_COMPACT=0). */
+int mv_get_stored_genes(mv_engine* e, int32_t* stored, int32_t* n_stored);
 /* Per-kernel timing of the last mv_attack_run when enabled (one state group then): HIP
  * events recorded on the run's stream around the row kernel(s), the classifier and
  * k_survive of every generation (summed ms). */

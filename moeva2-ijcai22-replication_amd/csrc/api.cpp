@@ -78,11 +78,41 @@ static unsigned short bf16_bits(float f) {
   return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 
+// Host copy of the problem and model descriptors: the engine builds its device tables from
+// it at creation (every gene stored) and again at mv_set_states for the compact layout.
+struct HostProblem {
+  int D = 0, V = 0, Dm = 0, C = 0, n_ohe = 0, n_pool = 0, norm = 2, scale_obj = 1;
+  double tol = 0.0;
+  std::vector<int> kind, feat, ohe_off, ohe_feats, mut, op_code, op_arg, pool;
+  std::vector<double> op_k, mls, mlm;
+};
+struct HostModel {
+  int n_layers = 0;
+  int dims[MAX_LAYERS + 1] = {};
+  std::vector<float> W[MAX_LAYERS], b[MAX_LAYERS];
+};
+
 struct mv_engine {
   int device = 0;
   int mlp_bf16 = 0;  // bf16 perf mode of the classifier tiles (mv_set_mlp_precision)
-  DProblem p{};
+  HostProblem hp;
+  HostModel hm;
+  DProblem p{};      // every gene stored: mv_evaluate / mv_decode / mv_variation, hosted loops
   std::vector<void*> prob_allocs;
+  // The attack's layout for the current state set (mv_set_states): compact when some genes
+  // can never change in any of the states (integer genes with xl == xu == their initial
+  // value); those are not stored in the pool, moved, mutated or summed.  ap() / as() / ag0()
+  // are what mv_attack_run reads.
+  bool compact = false;
+  std::vector<int> stored;           // the compact layout's stored genes
+  DProblem pc{};
+  std::vector<void*> compact_allocs;  // pc's tables (kept while the stored set is unchanged)
+  DStates sc{};
+  double* genes0c = nullptr;
+  std::vector<void*> cstate_allocs;
+  const DProblem& ap() const { return compact ? pc : p; }
+  const DStates& as() const { return compact ? sc : s; }
+  double* ag0() const { return compact ? genes0c : genes0; }
   float* W1full = nullptr;
   float* b1 = nullptr;
   int H1 = 0;
@@ -162,7 +192,9 @@ struct mv_engine {
     (void)hipSetDevice(device);
     if (xml) (void)hipFree(xml);
     free_list(attack_allocs);
+    free_list(cstate_allocs);
     free_list(state_allocs);
+    free_list(compact_allocs);
     free_list(prob_allocs);
     for (auto e : ev_var) (void)hipEventDestroy(e);
     for (auto e : ev_mlp) (void)hipEventDestroy(e);
@@ -176,6 +208,228 @@ struct mv_engine {
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
 };
+
+// The device tables of one gene layout.  keep: the stored genes (ascending indices into the
+// problem's V genes), or empty for all of them.  The draws stay defined over all V genes
+// (Vr, the gap table, the crossover subsets' sizes and every gene's subset index); cmap /
+// fidx (region B) translate.  A kept subset is only built for IDENT problems, where the
+// dropped genes' features are then simply immutable features: decoded from x_init, folded
+// into the per-state layer-1 bias, absent from f2's sum.
+static int build_problem(const HostProblem& h, const HostModel* hm, const std::vector<int>& keep,
+                         DProblem& p, std::vector<void*>& allocs) {
+  const int Vr = h.V, D = h.D, C = h.C;
+  std::vector<int> gk(keep);
+  if (gk.empty()) {
+    gk.resize(Vr);
+    std::iota(gk.begin(), gk.end(), 0);
+  }
+  const int V = (int)gk.size();
+  std::vector<int> sub_full(Vr), cmap(Vr, -1);
+  int ns[2] = {0, 0};
+  for (int g = 0; g < Vr; ++g) sub_full[g] = ns[h.kind[g] == MV_GENE_REAL ? 0 : 1]++;
+  std::vector<int> kind(V), feat(V), sub(V);
+  for (int c = 0; c < V; ++c) {
+    kind[c] = h.kind[gk[c]];
+    feat[c] = h.feat[gk[c]];
+    sub[c] = sub_full[gk[c]];
+    cmap[gk[c]] = c;
+  }
+  std::vector<int> mut(h.mut);
+  if ((int)gk.size() < Vr) mut = feat;  // IDENT: stored gene c <-> mutable feature c
+  const int Dm = (int)mut.size();
+  p = DProblem{};
+  p.D = D;
+  p.V = V;
+  p.Vr = Vr;
+  p.compact = V < Vr;
+  p.Dm = Dm;
+  p.Dm4 = (Dm + 15) & ~15;  // mutable features padded to a 16-k MFMA group
+  p.C = C;
+  p.n_ohe = h.n_ohe;
+  p.n_sub[0] = ns[0];
+  p.n_sub[1] = ns[1];
+  const int n_ohe_feats = h.n_ohe > 0 ? h.ohe_off[h.n_ohe] : 0;
+  p.n_ohe_feat = n_ohe_feats;
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err != hipSuccess) return;
+    err = upload(dst, host, n);
+    if (err == hipSuccess) allocs.push_back((void*)*dst);
+  };
+  K((int**)&p.gene_kind, kind.data(), V);
+  K((int**)&p.gene_feat, feat.data(), V);
+  K((int**)&p.gene_sub, sub.data(), V);
+  const int V4 = (V + 3) & ~3;
+  std::vector<int> info(V4, 0);
+  for (int c = 0; c < V; ++c) info[c] = kind[c] | (sub[c] << 2) | (feat[c] << 17);
+  K((int**)&p.gene_info, info.data(), V4);
+  K((int**)&p.ohe_off, h.ohe_off.data(), h.ohe_off.size());
+  K((int**)&p.ohe_feat, h.ohe_feats.data(), n_ohe_feats);
+  K((int**)&p.mut_feat, mut.data(), Dm);
+  {  // feature -> gene map of the decoder (mv_decode): -1 immutable, gene | (category+1) << 16
+    std::vector<int> fdec(D, -1);
+    for (int c = 0; c < V; ++c) {
+      if (kind[c] != MV_GENE_OHE) {
+        if (feat[c] >= 0 && feat[c] < D) fdec[feat[c]] = c;
+      } else {
+        const int q = feat[c];
+        for (int k = h.ohe_off[q]; k < h.ohe_off[q + 1]; ++k)
+          if (h.ohe_feats[k] >= 0 && h.ohe_feats[k] < D)
+            fdec[h.ohe_feats[k]] = c | ((k - h.ohe_off[q] + 1) << 16);
+      }
+    }
+    K((int**)&p.fdec, fdec.data(), D);
+  }
+  K((double**)&p.ml_scale, h.mls.data(), D);
+  K((double**)&p.ml_min, h.mlm.data(), D);
+  std::vector<double> ms(p.Dm4, 0.0), mm(p.Dm4, 0.0);
+  for (int j = 0; j < Dm; ++j) {
+    ms[j] = h.mls[mut[j]];
+    mm[j] = h.mlm[mut[j]];
+  }
+  K((double**)&p.mlS, ms.data(), p.Dm4);
+  K((double**)&p.mlM, mm.data(), p.Dm4);
+  // constraint program sorted by op code (lane-uniform branches), ABS_SUMDIFF ops last
+  std::vector<int> order(C);
+  for (int c = 0; c < C; ++c) order[c] = c;
+  auto key = [&](int c) { return h.op_code[c] == MV_OP_ABS_SUMDIFF ? 1 << 20 : h.op_code[c]; };
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key(x) < key(y); });
+  std::vector<int> scode(C), sarg((size_t)C * 4), scol(C);
+  std::vector<double> sk((size_t)C * 2);
+  int n_sd = 0;
+  for (int k = 0; k < C; ++k) {
+    const int c = order[k];
+    scode[k] = h.op_code[c];
+    scol[k] = c;
+    for (int q = 0; q < 4; ++q) sarg[(size_t)k * 4 + q] = h.op_arg[(size_t)c * 4 + q];
+    for (int q = 0; q < 2; ++q) sk[(size_t)k * 2 + q] = h.op_k[(size_t)c * 2 + q];
+    n_sd += scode[k] == MV_OP_ABS_SUMDIFF;
+  }
+  K((int**)&p.op_code, scode.data(), C);
+  K((int**)&p.op_arg, sarg.data(), (size_t)C * 4);
+  K((double**)&p.op_k, sk.data(), (size_t)C * 2);
+  K((int**)&p.op_col, scol.data(), C);
+  K((int**)&p.idx_pool, h.pool.data(), h.n_pool);
+  p.n_pool = h.n_pool;
+  p.n_sumdiff = n_sd;
+  p.full_ops = 0;
+  for (int c = 0; c < C; ++c)
+    if (h.op_code[c] >= MV_OP_LCLD_INSTALL && h.op_code[c] <= MV_OP_RATIO_MASKED) p.full_ops = 1;
+  p.ident = V == Dm;
+  for (int c = 0; c < V && p.ident; ++c) p.ident = kind[c] != MV_GENE_OHE && feat[c] == mut[c];
+  {  // k_vary problem blob: the LDS image of the tables (kernels.h vary_offsets)
+    const VaryOff vo = vary_offsets(p);
+    if (gen_lds(vo, false, false, true).total > 160 * 1024 || cons_lds_total(vo) > 160 * 1024)
+      return fail(MV_ERR_ARG, "problem too large for the k_vary LDS workspace");
+    std::vector<unsigned char> blob(vo.vb, 0);
+    auto put = [&](unsigned off, const void* src, size_t n) {
+      if (n) std::memcpy(blob.data() + off, src, n);
+    };
+    put(vo.opa, sarg.data(), (size_t)C * 16);
+    put(vo.opk, sk.data(), (size_t)C * 16);
+    put(vo.mlS, ms.data(), (size_t)p.Dm4 * 8);
+    put(vo.mlM, mm.data(), (size_t)p.Dm4 * 8);
+    put(vo.opc, scode.data(), (size_t)C * 4);
+    put(vo.ocol, scol.data(), (size_t)C * 4);
+    put(vo.pool, h.pool.data(), (size_t)h.n_pool * 4);
+    put(vo.ginfo, info.data(), (size_t)V4 * 4);
+    put(vo.mutf, mut.data(), (size_t)Dm * 4);
+    put(vo.ooff, h.ohe_off.data(), h.ohe_off.size() * 4);
+    if (n_ohe_feats > 0) put(vo.ofeat, h.ohe_feats.data(), (size_t)n_ohe_feats * 4);
+    put(vo.cmap, cmap.data(), (size_t)Vr * 4);
+    put(vo.fidx, gk.data(), (size_t)V * 4);
+    // mutation gap table T[k] = floor((1 - 1/Vr)^k 2^32), k = 0..Vr (oracle geometric_table)
+    std::vector<uint32_t> geo(Vr + 1);
+    const double q = 1.0 - 1.0 / (double)Vr;
+    for (int k = 0; k <= Vr; ++k) {
+      const double t = std::floor(std::pow(q, (double)k) * 4294967296.0);
+      geo[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    }
+    put(vo.geo, geo.data(), (size_t)(Vr + 1) * 4);
+    {  // region S: k_genc's slim program (kernels.h); the packed words mirror rowops pack_op
+      const int n_lane = C - n_sd;
+      p.slim = n_lane <= 64 * OPS_REG;
+      std::vector<double> k1(C);
+      std::vector<int> sd((size_t)(n_sd > 0 ? n_sd : 1) * 4, 0);
+      std::vector<unsigned> opw(C);
+      for (int k = 0; k < C; ++k) {
+        k1[k] = sk[(size_t)k * 2];
+        const int* ar = &sarg[(size_t)k * 4];
+        if (k < n_lane) {
+          p.slim &= (scode[k] == MV_OP_DIFF || scode[k] == MV_OP_RATIO_SAFE) && ar[0] >= 0 &&
+                    ar[0] < 0x4000 && ar[1] >= 0 && ar[1] < 0x4000;
+          opw[k] = (unsigned)scode[k] | ((unsigned)ar[0] << 4) | ((unsigned)ar[1] << 18);
+        } else {
+          opw[k] = 0u;
+          for (int q = 0; q < 4; ++q) sd[(size_t)(k - n_lane) * 4 + q] = ar[q];
+        }
+      }
+      put(vo.s_k, k1.data(), (size_t)C * 8);
+      put(vo.s_col, scol.data(), (size_t)C * 4);
+      put(vo.s_pool, h.pool.data(), (size_t)h.n_pool * 4);
+      put(vo.s_sd, sd.data(), sd.size() * 4);
+      put(vo.s_opw, opw.data(), (size_t)C * 4);
+      if (std::getenv("MV_SLIM") && std::getenv("MV_SLIM")[0] == '0') p.slim = 0;  // A/B
+    }
+    K((unsigned char**)&p.vblob, blob.data(), blob.size());
+  }
+  p.tol = h.tol;
+  p.norm = h.norm;
+  p.scale_obj = h.scale_obj;
+  p.f2_scale = h.norm == 2 ? 1.0 / (std::sqrt((double)D) - 0.0) : 1.0;
+  if (hm) {
+    p.n_layers = hm->n_layers;
+    for (int l = 0; l <= hm->n_layers; ++l) p.dims[l] = hm->dims[l];
+    const int H1 = hm->dims[1];
+    // layer 0: mutable rows, zero padded to Dm4
+    std::vector<float> w1m((size_t)p.Dm4 * H1, 0.f);
+    for (int j = 0; j < Dm; ++j)
+      std::memcpy(&w1m[(size_t)j * H1], hm->W[0].data() + (size_t)mut[j] * H1, H1 * sizeof(float));
+    K((float**)&p.W[0], w1m.data(), w1m.size());
+    for (int l = 1; l < hm->n_layers; ++l) {
+      K((float**)&p.W[l], hm->W[l].data(), (size_t)hm->dims[l] * hm->dims[l + 1]);
+      K((float**)&p.bias[l], hm->b[l].data(), hm->dims[l + 1]);
+    }
+    // k_mlp2 packing of the hidden layers: Wp[kg][n][16] = W[16 kg + i][n] (zero padded)
+    p.mlp2 = 1;
+    for (int l = 1; l < hm->n_layers; ++l) p.mlp2 &= hm->dims[l] % 16 == 0 && hm->dims[l] <= 128;
+    // xml_direct: k_mlp2 builds its layer-0 tiles from the child genes (MV_XML: the fp32
+    // ML rows written by the row kernel + k_mlp2, A/B only)
+    p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML");
+    for (int l = 0; l + 1 < hm->n_layers && p.mlp2; ++l) {
+      const int Kl = l == 0 ? p.Dm4 : hm->dims[l], Nl = hm->dims[l + 1];
+      const float* src = l == 0 ? w1m.data() : hm->W[l].data();  // [Kl][Nl] row-major
+      std::vector<float> wp((size_t)Kl * Nl, 0.f);
+      for (int k = 0; k < Kl; ++k)
+        for (int n = 0; n < Nl; ++n)
+          wp[((size_t)(k / 16) * Nl + n) * 16 + (k % 16)] = src[(size_t)k * Nl + n];
+      K((float**)&p.Wp[l], wp.data(), wp.size());
+    }
+    // bf16 perf mode packing of the MFMA layers: Wb[kg][n][32] = bf16(W[32 kg + i][n]), K
+    // zero padded to a multiple of 32 (engine.h DProblem::Wb)
+    for (int l = 0; l + 1 < hm->n_layers; ++l) {
+      const int Kl = l == 0 ? p.Dm4 : hm->dims[l], Nl = hm->dims[l + 1];
+      const int K32 = (Kl + 31) & ~31;
+      const float* src = l == 0 ? w1m.data() : hm->W[l].data();  // [Kl][Nl] row-major
+      std::vector<unsigned short> wb((size_t)K32 * Nl, 0);
+      for (int k = 0; k < Kl; ++k)
+        for (int n = 0; n < Nl; ++n)
+          wb[((size_t)(k / 32) * Nl + n) * 32 + (k % 32)] = bf16_bits(src[(size_t)k * Nl + n]);
+      K((unsigned short**)&p.Wb[l], wb.data(), wb.size());
+    }
+  } else {
+    p.n_layers = 0;
+  }
+  if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
+  if (hm) {
+    int hmax = 16;
+    for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
+    // the attack's classifier tiles (k_mlp / k_mlp2) read the mutable features only
+    const size_t lds = mlp_lds_bytes(p.Dm4, hmax, p.dims[p.n_layers - 1], p.dims[p.n_layers]);
+    if (lds > 160 * 1024) return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
+  }
+  return MV_OK;
+}
 
 extern "C" {
 
@@ -207,228 +461,70 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
   }
   for (int j = 1; j < Dm; ++j)
     if (pd->mut_feats[j] <= pd->mut_feats[j - 1]) return fail(MV_ERR_ARG, "mut_feats not ascending");
-  HIPCHK(hipSetDevice(device));
-  mv_engine* e = new mv_engine();
-  e->device = device;
-  DProblem& p = e->p;
-  p.D = D;
-  p.V = V;
-  p.Dm = Dm;
-  p.Dm4 = (Dm + 15) & ~15;  // mutable features padded to a 16-k MFMA group
-  p.C = C;
-  p.n_ohe = pd->n_ohe;
-  std::vector<int> sub(V);
   int ns[2] = {0, 0};
   for (int g = 0; g < V; ++g) {
     const int k = pd->gene_kind[g];
-    if (k < 0 || k > 2) {
-      delete e;
-      return fail(MV_ERR_ARG, "bad gene kind");
-    }
-    const int ss = k == MV_GENE_REAL ? 0 : 1;
-    sub[g] = ns[ss]++;
+    if (k < 0 || k > 2) return fail(MV_ERR_ARG, "bad gene kind");
+    const int sub = ns[k == MV_GENE_REAL ? 0 : 1]++;
+    if (pd->gene_feat[g] < 0 || pd->gene_feat[g] > 0x7FFF || sub > 0x7FFF)
+      return fail(MV_ERR_ARG, "feature/gene index too large for the packed gene table");
   }
-  p.n_sub[0] = ns[0];
-  p.n_sub[1] = ns[1];
-  std::vector<double> mls(D, 1.0), mlm(D, 0.0);
-  if (pd->ml_scale) std::memcpy(mls.data(), pd->ml_scale, D * sizeof(double));
-  if (pd->ml_min) std::memcpy(mlm.data(), pd->ml_min, D * sizeof(double));
+  if (V > VARY_MAX_V || ((Dm + 15) & ~15) > VARY_MAX_V)
+    return fail(MV_ERR_ARG, "genetic length / mutable features must be <= 1024");
+  HIPCHK(hipSetDevice(device));
+  mv_engine* e = new mv_engine();
+  e->device = device;
+  HostProblem& h = e->hp;
+  h.D = D;
+  h.V = V;
+  h.Dm = Dm;
+  h.C = C;
+  h.n_ohe = pd->n_ohe;
+  h.n_pool = pd->n_pool;
+  h.norm = pd->norm;
+  h.scale_obj = pd->scale_objectives;
+  h.tol = pd->tol;
+  h.kind.assign(pd->gene_kind, pd->gene_kind + V);
+  h.feat.assign(pd->gene_feat, pd->gene_feat + V);
+  h.ohe_off.assign(pd->n_ohe + 1, 0);
+  if (pd->n_ohe > 0) std::memcpy(h.ohe_off.data(), pd->ohe_offsets, (pd->n_ohe + 1) * sizeof(int));
   const int n_ohe_feats = pd->n_ohe > 0 ? pd->ohe_offsets[pd->n_ohe] : 0;
-  p.n_ohe_feat = n_ohe_feats;
-  std::vector<int> ohe_off(pd->n_ohe + 1, 0);
-  if (pd->n_ohe > 0) std::memcpy(ohe_off.data(), pd->ohe_offsets, (pd->n_ohe + 1) * sizeof(int));
+  h.ohe_feats.assign(pd->ohe_feats, pd->ohe_feats + n_ohe_feats);
+  h.mut.assign(pd->mut_feats, pd->mut_feats + Dm);
+  h.op_code.assign(pd->op_code, pd->op_code + C);
+  h.op_arg.assign(pd->op_arg, pd->op_arg + (size_t)C * 4);
+  h.op_k.assign(pd->op_karg, pd->op_karg + (size_t)C * 2);
+  h.pool.assign(pd->idx_pool, pd->idx_pool + pd->n_pool);
+  h.mls.assign(D, 1.0);
+  h.mlm.assign(D, 0.0);
+  if (pd->ml_scale) std::memcpy(h.mls.data(), pd->ml_scale, D * sizeof(double));
+  if (pd->ml_min) std::memcpy(h.mlm.data(), pd->ml_min, D * sizeof(double));
+  if (md) {
+    e->has_model = true;
+    HostModel& m = e->hm;
+    m.n_layers = md->n_layers;
+    for (int l = 0; l <= md->n_layers; ++l) m.dims[l] = md->dims[l];
+    for (int l = 0; l < md->n_layers; ++l) {
+      m.W[l].assign(md->W[l], md->W[l] + (size_t)md->dims[l] * md->dims[l + 1]);
+      m.b[l].assign(md->b[l], md->b[l] + md->dims[l + 1]);
+    }
+  }
+  const int rc = build_problem(h, md ? &e->hm : nullptr, {}, e->p, e->prob_allocs);
+  if (rc != MV_OK) {
+    delete e;
+    return rc;
+  }
+  // layer-1 bias fold of k_setup_states: the full W0 (feature rows) and b1
   hipError_t err = hipSuccess;
   auto K = [&](auto** dst, const auto* host, size_t n) {
     if (err == hipSuccess) err = e->keep(e->prob_allocs, dst, host, n);
   };
-  K((int**)&p.gene_kind, pd->gene_kind, V);
-  K((int**)&p.gene_feat, pd->gene_feat, V);
-  K((int**)&p.gene_sub, sub.data(), V);
-  const int V4 = (V + 3) & ~3;
-  std::vector<int> info(V4, 0);
-  for (int g = 0; g < V; ++g) {
-    if (pd->gene_feat[g] < 0 || pd->gene_feat[g] > 0x7FFF || sub[g] > 0x7FFF) {
-      delete e;
-      return fail(MV_ERR_ARG, "feature/gene index too large for the packed gene table");
-    }
-    info[g] = pd->gene_kind[g] | (sub[g] << 2) | (pd->gene_feat[g] << 17);
-  }
-  K((int**)&p.gene_info, info.data(), V4);
-  K((int**)&p.ohe_off, ohe_off.data(), ohe_off.size());
-  K((int**)&p.ohe_feat, pd->ohe_feats, n_ohe_feats);
-  K((int**)&p.mut_feat, pd->mut_feats, Dm);
-  {  // feature -> gene map of the decoder (mv_decode): -1 immutable, gene | (category+1) << 16
-    std::vector<int> fdec(D, -1);
-    for (int g = 0; g < V; ++g) {
-      if (pd->gene_kind[g] != MV_GENE_OHE) {
-        if (pd->gene_feat[g] >= 0 && pd->gene_feat[g] < D) fdec[pd->gene_feat[g]] = g;
-      } else {
-        const int q = pd->gene_feat[g];
-        for (int k = pd->ohe_offsets[q]; k < pd->ohe_offsets[q + 1]; ++k)
-          if (pd->ohe_feats[k] >= 0 && pd->ohe_feats[k] < D)
-            fdec[pd->ohe_feats[k]] = g | ((k - pd->ohe_offsets[q] + 1) << 16);
-      }
-    }
-    K((int**)&p.fdec, fdec.data(), D);
-  }
-  K((double**)&p.ml_scale, mls.data(), D);
-  K((double**)&p.ml_min, mlm.data(), D);
-  {
-    const int Dm4 = p.Dm4;
-    std::vector<double> ms(Dm4, 0.0), mm(Dm4, 0.0);
-    for (int j = 0; j < Dm; ++j) {
-      ms[j] = mls[pd->mut_feats[j]];
-      mm[j] = mlm[pd->mut_feats[j]];
-    }
-    K((double**)&p.mlS, ms.data(), Dm4);
-    K((double**)&p.mlM, mm.data(), Dm4);
-  }
-  // constraint program sorted by op code (lane-uniform branches), ABS_SUMDIFF ops last
-  std::vector<int> order(C);
-  for (int c = 0; c < C; ++c) order[c] = c;
-  auto key = [&](int c) { return pd->op_code[c] == MV_OP_ABS_SUMDIFF ? 1 << 20 : pd->op_code[c]; };
-  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key(x) < key(y); });
-  std::vector<int> scode(C), sarg((size_t)C * 4), scol(C);
-  std::vector<double> sk((size_t)C * 2);
-  int n_sd = 0;
-  for (int k = 0; k < C; ++k) {
-    const int c = order[k];
-    scode[k] = pd->op_code[c];
-    scol[k] = c;
-    for (int q = 0; q < 4; ++q) sarg[(size_t)k * 4 + q] = pd->op_arg[(size_t)c * 4 + q];
-    for (int q = 0; q < 2; ++q) sk[(size_t)k * 2 + q] = pd->op_karg[(size_t)c * 2 + q];
-    n_sd += scode[k] == MV_OP_ABS_SUMDIFF;
-  }
-  K((int**)&p.op_code, scode.data(), C);
-  K((int**)&p.op_arg, sarg.data(), (size_t)C * 4);
-  K((double**)&p.op_k, sk.data(), (size_t)C * 2);
-  K((int**)&p.op_col, scol.data(), C);
-  K((int**)&p.idx_pool, pd->idx_pool, pd->n_pool);
-  p.n_pool = pd->n_pool;
-  p.n_sumdiff = n_sd;
-  p.full_ops = 0;
-  for (int c = 0; c < C; ++c)
-    if (pd->op_code[c] >= MV_OP_LCLD_INSTALL && pd->op_code[c] <= MV_OP_RATIO_MASKED)
-      p.full_ops = 1;
-  p.ident = V == Dm;
-  for (int g = 0; g < V && p.ident; ++g)
-    p.ident = pd->gene_kind[g] != MV_GENE_OHE && pd->gene_feat[g] == pd->mut_feats[g];
-  if (V > VARY_MAX_V || p.Dm4 > VARY_MAX_V) {
-    delete e;
-    return fail(MV_ERR_ARG, "genetic length / mutable features must be <= 1024");
-  }
-  {  // k_vary problem blob: the LDS image of the tables (kernels.h vary_offsets)
-    const VaryOff vo = vary_offsets(p);
-    if (gen_lds(vo, false, false, true).total > 160 * 1024 || cons_lds_total(vo) > 160 * 1024) {
-      delete e;
-      return fail(MV_ERR_ARG, "problem too large for the k_vary LDS workspace");
-    }
-    std::vector<unsigned char> blob(vo.vb, 0);
-    auto put = [&](unsigned off, const void* src, size_t n) {
-      if (n) std::memcpy(blob.data() + off, src, n);
-    };
-    put(vo.opa, sarg.data(), (size_t)C * 16);
-    put(vo.opk, sk.data(), (size_t)C * 16);
-    std::vector<double> ms(p.Dm4, 0.0), mm(p.Dm4, 0.0);
-    for (int j = 0; j < Dm; ++j) {
-      ms[j] = mls[pd->mut_feats[j]];
-      mm[j] = mlm[pd->mut_feats[j]];
-    }
-    put(vo.mlS, ms.data(), (size_t)p.Dm4 * 8);
-    put(vo.mlM, mm.data(), (size_t)p.Dm4 * 8);
-    put(vo.opc, scode.data(), (size_t)C * 4);
-    put(vo.ocol, scol.data(), (size_t)C * 4);
-    put(vo.pool, pd->idx_pool, (size_t)pd->n_pool * 4);
-    put(vo.ginfo, info.data(), (size_t)V4 * 4);
-    put(vo.mutf, pd->mut_feats, (size_t)Dm * 4);
-    put(vo.ooff, ohe_off.data(), ohe_off.size() * 4);
-    if (n_ohe_feats > 0) put(vo.ofeat, pd->ohe_feats, (size_t)n_ohe_feats * 4);
-    // mutation gap table T[k] = floor((1 - 1/V)^k 2^32), k = 0..V (oracle geometric_table)
-    std::vector<uint32_t> geo(V + 1);
-    const double q = 1.0 - 1.0 / (double)V;
-    for (int k = 0; k <= V; ++k) {
-      const double t = std::floor(std::pow(q, (double)k) * 4294967296.0);
-      geo[k] = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-    }
-    put(vo.geo, geo.data(), (size_t)(V + 1) * 4);
-    {  // region S: k_genc's slim program (kernels.h); the packed words mirror rowops pack_op
-      const int n_lane = C - n_sd;
-      p.slim = n_lane <= 64 * OPS_REG;
-      std::vector<double> k1(C);
-      std::vector<int> sd((size_t)(n_sd > 0 ? n_sd : 1) * 4, 0);
-      std::vector<unsigned> opw(C);
-      for (int k = 0; k < C; ++k) {
-        k1[k] = sk[(size_t)k * 2];
-        const int* ar = &sarg[(size_t)k * 4];
-        if (k < n_lane) {
-          p.slim &= (scode[k] == MV_OP_DIFF || scode[k] == MV_OP_RATIO_SAFE) && ar[0] >= 0 &&
-                    ar[0] < 0x4000 && ar[1] >= 0 && ar[1] < 0x4000;
-          opw[k] = (unsigned)scode[k] | ((unsigned)ar[0] << 4) | ((unsigned)ar[1] << 18);
-        } else {
-          opw[k] = 0u;
-          for (int q = 0; q < 4; ++q) sd[(size_t)(k - n_lane) * 4 + q] = ar[q];
-        }
-      }
-      put(vo.s_k, k1.data(), (size_t)C * 8);
-      put(vo.s_col, scol.data(), (size_t)C * 4);
-      put(vo.s_pool, pd->idx_pool, (size_t)pd->n_pool * 4);
-      put(vo.s_sd, sd.data(), sd.size() * 4);
-      put(vo.s_opw, opw.data(), (size_t)C * 4);
-      if (std::getenv("MV_SLIM") && std::getenv("MV_SLIM")[0] == '0') p.slim = 0;  // A/B
-    }
-    K((unsigned char**)&p.vblob, blob.data(), blob.size());
-  }
-  p.tol = pd->tol;
-  p.norm = pd->norm;
-  p.scale_obj = pd->scale_objectives;
-  p.f2_scale = pd->norm == 2 ? 1.0 / (std::sqrt((double)D) - 0.0) : 1.0;
   if (md) {
-    e->has_model = true;
-    p.n_layers = md->n_layers;
-    for (int l = 0; l <= md->n_layers; ++l) p.dims[l] = md->dims[l];
     e->H1 = md->dims[1];
-    // layer 0: mutable rows, zero padded to Dm4
-    std::vector<float> w1m((size_t)p.Dm4 * e->H1, 0.f);
-    for (int j = 0; j < Dm; ++j)
-      std::memcpy(&w1m[(size_t)j * e->H1], md->W[0] + (size_t)pd->mut_feats[j] * e->H1,
-                  e->H1 * sizeof(float));
-    K((float**)&p.W[0], w1m.data(), w1m.size());
     K(&e->W1full, md->W[0], (size_t)D * e->H1);
     K(&e->b1, md->b[0], e->H1);
-    p.bias[0] = e->b1;
-    for (int l = 1; l < md->n_layers; ++l) {
-      K((float**)&p.W[l], md->W[l], (size_t)md->dims[l] * md->dims[l + 1]);
-      K((float**)&p.bias[l], md->b[l], md->dims[l + 1]);
-    }
-    // k_mlp2 packing of the hidden layers: Wp[kg][n][16] = W[16 kg + i][n] (zero padded)
-    p.mlp2 = 1;
-    for (int l = 1; l < md->n_layers; ++l) p.mlp2 &= md->dims[l] % 16 == 0 && md->dims[l] <= 128;
-    // xml_direct: k_mlp2 builds its layer-0 tiles from the child genes (MV_XML: the fp32
-    // ML rows written by the row kernel + k_mlp2, A/B only)
-    p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML");
-    for (int l = 0; l + 1 < md->n_layers && p.mlp2; ++l) {
-      const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
-      const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major
-      std::vector<float> wp((size_t)Kl * Nl, 0.f);
-      for (int k = 0; k < Kl; ++k)
-        for (int n = 0; n < Nl; ++n)
-          wp[((size_t)(k / 16) * Nl + n) * 16 + (k % 16)] = src[(size_t)k * Nl + n];
-      K((float**)&p.Wp[l], wp.data(), wp.size());
-    }
-    // bf16 perf mode packing of the MFMA layers: Wb[kg][n][32] = bf16(W[32 kg + i][n]), K
-    // zero padded to a multiple of 32 (engine.h DProblem::Wb)
-    for (int l = 0; l + 1 < md->n_layers; ++l) {
-      const int Kl = l == 0 ? p.Dm4 : md->dims[l], Nl = md->dims[l + 1];
-      const int K32 = (Kl + 31) & ~31;
-      const float* src = l == 0 ? w1m.data() : md->W[l];  // [Kl][Nl] row-major
-      std::vector<unsigned short> wb((size_t)K32 * Nl, 0);
-      for (int k = 0; k < Kl; ++k)
-        for (int n = 0; n < Nl; ++n)
-          wb[((size_t)(k / 32) * Nl + n) * 32 + (k % 32)] = bf16_bits(src[(size_t)k * Nl + n]);
-      K((unsigned short**)&p.Wb[l], wb.data(), wb.size());
-    }
+    e->p.bias[0] = e->b1;
   } else {
-    p.n_layers = 0;
     e->H1 = 16;
     std::vector<float> zero(16, 0.f);
     K(&e->W1full, zero.data(), 16);
@@ -438,23 +534,56 @@ int mv_engine_create(int32_t device, const mv_problem_desc* pd, const mv_model_d
     delete e;
     return fail(MV_ERR_HIP, std::string("upload: ") + hipGetErrorString(err));
   }
-  if (md) {
-    int hmax = 16;
-    for (int l = 1; l < p.n_layers; ++l) hmax = p.dims[l] > hmax ? p.dims[l] : hmax;
-    // the attack's classifier tiles (k_mlp / k_mlp2) read the mutable features only
-    const size_t lds = mlp_lds_bytes(p.Dm4, hmax, p.dims[p.n_layers - 1], p.dims[p.n_layers]);
-    if (lds > 160 * 1024) {
-      delete e;
-      return fail(MV_ERR_ARG, "problem too large for the evaluation tile (LDS)");
-    }
-  }
   *out = e;
   return MV_OK;
 }
 
 void mv_engine_destroy(mv_engine* e) { delete e; }
 
-static RowsArgs base_rows(const mv_engine* e);
+// attack: the attack's layout (compact when mv_set_states found fixed genes)
+static RowsArgs base_rows(const mv_engine* e, bool attack = false);
+
+// The genes no attack on this state set can change: integer genes (not one-hot) whose
+// bounds are equal and whose initial value -- x_init, already integral -- is that bound in
+// every state (crossover swaps equal values, a mutation is clamped back to the bound).  Such
+// genes exist only in IDENT problems here (botnet: 120 of 432); MV_COMPACT=0 keeps them all.
+// Returns the genes to store (ascending), or empty when every gene is stored.
+static std::vector<int> stored_genes(const mv_engine* e, int B, const double* x_init,
+                                     const double* xl, const double* xu) {
+  const HostProblem& h = e->hp;
+  std::vector<int> keep;
+  const char* env = std::getenv("MV_COMPACT");
+  if ((env && env[0] == '0') || !e->p.ident || !e->has_model) return keep;
+  for (int g = 0; g < h.V; ++g) {
+    bool fixed = h.kind[g] == MV_GENE_INT;
+    const int f = h.feat[g];
+    for (int b = 0; b < B && fixed; ++b) {
+      const double x = x_init[(size_t)b * h.D + f], lo = xl[(size_t)b * h.D + f],
+                   hi = xu[(size_t)b * h.D + f];
+      fixed = lo == hi && x == lo && std::rint(x) == x;
+    }
+    if (!fixed) keep.push_back(g);
+  }
+  if ((int)keep.size() == h.V || keep.empty()) keep.clear();
+  return keep;
+}
+
+static hipError_t alloc_states(mv_engine* e, const DProblem& p, int B, const double* x_init,
+                               std::vector<void*>& list, DStates& s, double*& genes0) {
+  s = DStates{};
+  s.B = B;
+  hipError_t err = hipSuccess;
+  auto K = [&](auto** dst, const auto* host, size_t n) {
+    if (err == hipSuccess) err = e->keep(list, dst, host, n);
+  };
+  K((double**)&s.x_init, x_init, (size_t)B * p.D);
+  K((double**)&s.gl, (const double*)nullptr, (size_t)B * p.V);
+  K((double**)&s.gu, (const double*)nullptr, (size_t)B * p.V);
+  K((unsigned char**)&s.sblob, (const unsigned char*)nullptr, (size_t)B * vary_offsets(p).sb);
+  K((float**)&s.bias1, (const float*)nullptr, (size_t)B * e->H1);
+  K(&genes0, (const double*)nullptr, (size_t)B * p.V);
+  return err;
+}
 
 int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* xl,
                   const double* xu, const int32_t* minimize_class, void* stream) {
@@ -467,50 +596,63 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
     if (minimize_class[b] < 0 || minimize_class[b] >= nout)
       return fail(MV_ERR_ARG, "minimize_class out of range");
   HIPCHK(hipDeviceSynchronize());
+  e->free_list(e->cstate_allocs);
   e->free_list(e->state_allocs);
   e->free_list(e->attack_allocs);
   e->d_phase = nullptr;
   e->attack_ready = false;
-  const DProblem& p = e->p;
-  DStates& s = e->s;
-  s.B = B;
+  e->compact = false;
+  e->B = 0;
   double *dxl = nullptr, *dxu = nullptr;
-  hipError_t err = hipSuccess;
-  auto K = [&](auto** dst, const auto* host, size_t n) {
-    if (err == hipSuccess) err = e->keep(e->state_allocs, dst, host, n);
-  };
-  K((double**)&s.x_init, x_init, (size_t)B * p.D);
-  K(&dxl, xl, (size_t)B * p.D);
-  K(&dxu, xu, (size_t)B * p.D);
-  K((int**)&s.min_class, minimize_class, B);
-  K((double**)&s.gl, (const double*)nullptr, (size_t)B * p.V);
-  K((double**)&s.gu, (const double*)nullptr, (size_t)B * p.V);
-  K((unsigned char**)&s.sblob, (const unsigned char*)nullptr,
-    (size_t)B * vary_offsets(p).sb);
-  K((float**)&s.bias1, (const float*)nullptr, (size_t)B * e->H1);
-  K(&e->genes0, (const double*)nullptr, (size_t)B * p.V);
+  hipError_t err = alloc_states(e, e->p, B, x_init, e->state_allocs, e->s, e->genes0);
+  if (err == hipSuccess) err = e->keep(e->state_allocs, &dxl, xl, (size_t)B * e->p.D);
+  if (err == hipSuccess) err = e->keep(e->state_allocs, &dxu, xu, (size_t)B * e->p.D);
+  if (err == hipSuccess)
+    err = e->keep(e->state_allocs, (int**)&e->s.min_class, minimize_class, (size_t)B);
   if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
   int slot = 0;
   HIPCHK(stage_rows(base_rows(e), (hipStream_t)stream, &slot));
-  HIPCHK(launch_setup_states(slot, B, s.x_init, dxl, dxu, e->W1full, e->b1, (double*)s.gl,
-                             (double*)s.gu, (unsigned char*)s.sblob, (float*)s.bias1, e->genes0,
-                             (hipStream_t)stream));
+  HIPCHK(launch_setup_states(slot, B, e->s.x_init, dxl, dxu, e->W1full, e->b1, (double*)e->s.gl,
+                             (double*)e->s.gu, (unsigned char*)e->s.sblob, (float*)e->s.bias1,
+                             e->genes0, (hipStream_t)stream));
   HIPCHK(release_rows(slot, (hipStream_t)stream));
+  // the attack's compact layout, when this state set has genes that never change
+  const std::vector<int> keep = stored_genes(e, B, x_init, xl, xu);
+  if (!keep.empty()) {
+    if (keep != e->stored) {
+      HIPCHK(hipDeviceSynchronize());
+      e->free_list(e->compact_allocs);
+      e->stored.clear();
+      const int rc = build_problem(e->hp, e->has_model ? &e->hm : nullptr, keep, e->pc,
+                                   e->compact_allocs);
+      if (rc != MV_OK) return rc;
+      e->pc.bias[0] = e->b1;
+      e->stored = keep;
+    }
+    err = alloc_states(e, e->pc, B, x_init, e->cstate_allocs, e->sc, e->genes0c);
+    if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
+    e->sc.min_class = e->s.min_class;
+    e->compact = true;
+    HIPCHK(stage_rows(base_rows(e, true), (hipStream_t)stream, &slot));
+    HIPCHK(launch_setup_states(slot, B, e->sc.x_init, dxl, dxu, e->W1full, e->b1,
+                               (double*)e->sc.gl, (double*)e->sc.gu, (unsigned char*)e->sc.sblob,
+                               (float*)e->sc.bias1, e->genes0c, (hipStream_t)stream));
+    HIPCHK(release_rows(slot, (hipStream_t)stream));
+  }
   e->B = B;
   return MV_OK;
 }
 
-static RowsArgs base_rows(const mv_engine* e) {
+static RowsArgs base_rows(const mv_engine* e, bool attack) {
   RowsArgs a{};
-  a.p = e->p;
-  a.s = e->s;
+  a.p = attack ? e->ap() : e->p;
+  a.s = attack ? e->as() : e->s;
   a.eta = 20.0;
   a.cx_prob = e->cx_prob;
   a.cx_kind = e->cx_kind;
   a.sbx_eta = e->sbx_eta;
   a.state_keys = e->state_keys;
   a.key0 = e->key0;
-  a.mut_thr = (uint32_t)(4294967296.0 / (double)e->p.V);
   a.do_eval = 1;
   a.p.mlp_bf16 = e->has_model && e->mlp_bf16;
   return a;
@@ -667,8 +809,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   }
   hipStream_t stream = (hipStream_t)stream_;
   HIPCHK(hipSetDevice(e->device));
-  const int B = e->B, V = e->p.V, S = P + O;
-  const int hist_w = prm->history == 2 ? 3 + e->p.C : 3;
+  const DProblem& ap = e->ap();  // the attack's layout (compact: fixed genes not stored)
+  const int B = e->B, V = ap.V, S = P + O;
+  const int hist_w = prm->history == 2 ? 3 + ap.C : 3;
   const int hist_rows = P + (G - 1) * O;
   const bool realloc = !e->attack_ready || e->P != P || e->O != O || e->R != R ||
                        e->hist_mode != prm->history || e->n_gen != G;
@@ -730,7 +873,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
                      (double)-INFINITY);
   hipLaunchKernelGGL(k_fill_i, dim3(64), dim3(256), 0, stream, e->has_ext, (size_t)B, 0);
   HIPCHK(hipGetLastError());
-  HIPCHK(launch_init_pool(B, P, O, V, S, e->genes0, e->pool, e->pop_slot, e->free_slot, stream));
+  HIPCHK(launch_init_pool(B, P, O, V, S, e->ag0(), e->pool, e->pop_slot, e->free_slot, stream));
   HIPCHK(e->ensure_xml((size_t)B * (P > O ? P : O)));
   // Initial states are independent: split them into state groups, each running its own
   // generation chain on its own stream, so one group's latency-bound survival overlaps the
@@ -752,9 +895,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     gs[q] = e->streams[q];
     HIPCHK(hipStreamWaitEvent(gs[q], e->ev_fork, 0));
   }
-  const int H1 = e->H1, D = e->p.D;
-  const unsigned sbb = vary_offsets(e->p).sb;
-  const size_t Dm4 = e->p.Dm4;
+  const int H1 = e->H1, D = ap.D;
+  const unsigned sbb = vary_offsets(ap).sb;
+  const size_t Dm4 = ap.Dm4;
   auto group_rows = [&](RowsArgs r, int q, int n_per_state) {
     const size_t b0 = gb0[q];
     r.s.B = gb0[q + 1] - gb0[q];
@@ -795,7 +938,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     return s;
   };
   // initial population evaluation (pymoo _initialize)
-  RowsArgs ev = base_rows(e);
+  RowsArgs ev = base_rows(e, true);
   ev.n = P;
   ev.mode = 0;
   ev.genes_in = e->pool;
@@ -856,7 +999,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   }
   e->n_var_rec = 0;
   e->n_surv_rec = 0;
-  RowsArgs va = base_rows(e);
+  RowsArgs va = base_rows(e, true);
   va.n = O;
   va.mode = 1;
   va.genes_in = e->pool;
@@ -920,7 +1063,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
 
 int mv_get_row_kernel(mv_engine* e, int32_t* kind) {
   if (!e || !kind) return fail(MV_ERR_ARG, "null argument");
-  RowsArgs a = base_rows(e);
+  RowsArgs a = base_rows(e, true);
   a.n = 2;
   a.total = 2;
   a.mode = 1;
@@ -930,7 +1073,7 @@ int mv_get_row_kernel(mv_engine* e, int32_t* kind) {
 
 int mv_get_mlp_kernel(mv_engine* e, int32_t* kind) {
   if (!e || !kind) return fail(MV_ERR_ARG, "null argument");
-  *kind = mlp_kernel_kind(base_rows(e).p);
+  *kind = mlp_kernel_kind(base_rows(e, true).p);
   return MV_OK;
 }
 
@@ -1365,8 +1508,11 @@ int mv_debug_survival_dump(double* out) {
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
   if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
   HIPCHK(hipSetDevice(e->device));
-  HIPCHK(launch_gather_pop(e->B, e->P, e->p.V, e->S, e->pop_slot, e->pool, e->poolF, genes, F,
-                           (hipStream_t)stream));
+  // the pool's rows in the attack's layout -> genes of every one of the Vr genes
+  const DProblem& ap = e->ap();
+  const int* cmap = ap.compact ? (const int*)(ap.vblob + vary_offsets(ap).cmap) : nullptr;
+  HIPCHK(launch_gather_pop(e->B, e->P, ap.V, ap.Vr, e->S, cmap, e->s.gl, e->pop_slot, e->pool,
+                           e->poolF, genes, F, (hipStream_t)stream));
   if (MV_CHECKS_ON) {  // checks build: a failed device index check fails the attack loudly
     int32_t r[8];
     if (mv_debug_checks(r, nullptr) != MV_OK) return MV_ERR_HIP;
@@ -1377,6 +1523,18 @@ int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
                                     std::to_string(r[4]) + ", " + std::to_string(r[5]) +
                                     " failures)");
   }
+  return MV_OK;
+}
+
+int mv_get_stored_genes(mv_engine* e, int32_t* stored, int32_t* n_stored) {
+  if (!e || !n_stored) return fail(MV_ERR_ARG, "null argument");
+  const DProblem& ap = e->ap();
+  *n_stored = ap.V;
+  if (stored)
+    for (int g = 0; g < ap.Vr; ++g) {
+      const auto it = std::lower_bound(e->stored.begin(), e->stored.end(), g);
+      stored[g] = !ap.compact || (it != e->stored.end() && *it == g);
+    }
   return MV_OK;
 }
 

@@ -50,12 +50,19 @@ constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound 
 
 struct DProblem {
   int D, V, Dm, Dm4, C, n_ohe;  // Dm4: mutable features padded to a multiple of 16
+  // Vr: the genetic length the variation draws are defined over (mutation positions, SBX
+  // draw indices, the geometric gap table).  V = Vr except in the attack's compact layout
+  // (mv_set_states): there the genes that can never change -- integer genes whose bounds are
+  // equal and whose initial value is that bound in every state -- are not stored; V counts
+  // the free genes, and region B's cmap / fidx map between the two numberings
+  int Vr;
   int n_ohe_feat;         // features of all one-hot groups (ohe_feat length)
-  int n_sub[2];           // crossover subsets: 0 real, 1 int (OHE genes are int)
+  int n_sub[2];           // crossover subsets: 0 real, 1 int (OHE genes are int), over Vr
   const int* gene_kind;   // [V]
   const int* gene_feat;   // [V]
-  const int* gene_sub;    // [V] index within its subset
+  const int* gene_sub;    // [V] index within its subset (of the full Vr genes)
   const int* gene_info;   // [V4] kind | sub << 2 | feat << 17 (zero padded to a multiple of 4)
+  int compact;            // V < Vr: the compact layout (cmap / fidx are not identities)
   const int* ohe_off;     // [n_ohe+1]
   const int* ohe_feat;
   const int* mut_feat;    // [Dm]
@@ -139,7 +146,6 @@ struct RowsArgs {
   uint32_t stream_key;
   int state_keys;           // 1: state b draws from stream stream_key + key0 + b (per-state
   uint32_t key0;            //    streams, mv_set_state_streams); 0: every state shares stream_key
-  uint32_t mut_thr;         // floor(2^32 / V)
   double eta;               // 20
   double cx_prob;           // 0.9
   int cx_kind;              // 0: two-point (the reference), 1: SBX (north_star option)

@@ -97,11 +97,12 @@ template <int CAP, class Preload>
 __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, const int b,
                                           const int irow, const bool mine, const int gen,
                                           const bool sbx, const uint32_t* geo, const int* ginfo,
-                                          const double* gin, const Rng& rng, int& par_v,
+                                          const int* cmap, const double* gin, const Rng& rng,
+                                          int& par_v,
                                           int& cx0_v, int& cx1_v, int& mut_v, int (&mpos)[CAP],
                                           double (&mval)[CAP], const int2 pre_pr,
                                           Preload&& preload) {
-  const int V = p.V;
+  const int V = p.V, Vr = p.Vr;  // stored genes, genes the draws are defined over
   if (mine) {
     const int nm = a.n / 2;
     const int m = irow % nm;
@@ -116,8 +117,8 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
     }
   }
   preload();
-  // (1) mutation positions and their PM uniforms
-  const float lq = __log2f(1.0f - 1.0f / (float)V);
+  // (1) mutation positions (of the Vr genes) and their PM uniforms
+  const float lq = __log2f(1.0f - 1.0f / (float)Vr);
   bool going = mine && !sbx;
   int pos = -1, cnt = 0, ovf = 0;
   double mu[CAP] = {};
@@ -127,8 +128,8 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
     double u = 0.0;
     if (going) {
       const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-      pos += 1 + geo_gap(geo, V, w.x, lq);
-      if (pos >= V) {
+      pos += 1 + geo_gap(geo, Vr, w.x, lq);
+      if (pos >= Vr) {
         going = false;
       } else if (j == CAP) {
         ovf = 1;
@@ -149,6 +150,9 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   // (2) + (3) one (row, mutation) pair per lane: lane 4 k + q loads row k's crossed parent
   // value and gene bounds at its q-th mutated position and mutates it -- one pow pair deep
   // instead of a loop over the wave's largest mutation count (a wave holds <= 16 rows).
+  // The position is mapped to its stored gene (cmap); a fixed gene of the compact layout
+  // (-1) is not stored and its mutation is the identity (integer gene, xl == xu == value),
+  // so the row keeps the draw and drops the write.
   static_assert(CAP == 4, "row_draws maps 16 rows x 4 mutations onto the 64 lanes");
   const double* gl = a.s.gl + (size_t)b * V;
   const double* gu = a.s.gu + (size_t)b * V;
@@ -167,19 +171,23 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   }
   const int cntk = __shfl(cnt, kk), park = __shfl(par_v, kk);
   const int c0k = __shfl(cx0_v, kk), c1k = __shfl(cx1_v, kk);
-  const int mp = MV_IDX(pq < 0 ? 0 : pq, V, CK_GEN_MUTPOS);  // unconditional, clamped loads
+  const int cq = cmap[MV_IDX(pq < 0 ? 0 : pq, Vr, CK_GEN_MUTPOS)];  // unconditional loads
+  const int mp = MV_IDX(cq < 0 ? 0 : cq, V, CK_GEN_MUTPOS);
   const int gi = ginfo[mp];
   const int mrow = MV_IDX(swapped_packed(gi, c0k, c1k) ? (park >> 16) : (park & 0xFFFF),
                           a.in_rows, CK_GEN_MUTROW);
   double xv = gin[MV_IDX((size_t)mrow * V + mp, (long long)a.in_rows * V, CK_AT_MUTLOAD)];
   const double lo = gl[MV_IDX(mp, V, CK_AT_BOUNDS)], hi = gu[MV_IDX(mp, V, CK_AT_BOUNDS)];
   if (qq < cntk) xv = mutate_gene(xv, lo, hi, (gi & 3) == 0, uq, a.eta);
-#pragma unroll
-  for (int q = 0; q < CAP; ++q) mval[q] = __shfl(xv, (lane * 4 + q) & 63);  // back to row lanes
   int last = -1;
 #pragma unroll
   for (int q = 0; q < CAP; ++q)
     if (q < cnt) last = mpos[q];
+#pragma unroll
+  for (int q = 0; q < CAP; ++q) {  // back to the row lanes: values and stored positions
+    mval[q] = __shfl(xv, (lane * 4 + q) & 63);
+    mpos[q] = __shfl(cq, (lane * 4 + q) & 63);
+  }
   mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
 }
 
@@ -260,6 +268,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
   const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
   const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
+  const int* s_cmap = (const int*)(smem + L.b_at + (o.cmap - o.b_at));
+  const int* s_fidx = (const int*)(smem + L.b_at + (o.fidx - o.b_at));
   const double* s_mlS = (const double*)(smem + L.c_at + (o.mlS - o.c_at));
   const double* s_mlM = (const double*)(smem + L.c_at + (o.mlM - o.c_at));
   const double* s_es = (const double*)(smem + L.e_at + (o.es - o.e_at));
@@ -301,8 +311,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (nrw > 1) load_row(1, xb);
   };
   if (a.mode == 1) {
-    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, gin, rng, par_v, cx0_v,
-                       cx1_v, mut_v, mpos, mval, pre_pr, preload);
+    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, s_cmap, gin, rng, par_v,
+                       cx0_v, cx1_v, mut_v, mpos, mval, pre_pr, preload);
   } else {
     if (mine) par_v = irow | (irow << 16);
     preload();
@@ -391,9 +401,9 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       const int pr = rdl(par_v, k);
       unsigned char* sb = smem + gen_sbx_at(L) + (size_t)wave * gen_sbx_wave_bytes(NT);
       sbx_row<NT>(x, ginf, gin + (size_t)(pr & 0xFFFF) * V, gin + (size_t)(pr >> 16) * V, sgl,
-                  sgu, V, i % nm, i / nm, rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen,
+                  sgu, V, s_fidx, i % nm, i / nm, rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen,
                   a.sbx_eta, lane, (int*)(sb + 64 * NT * 8), (double*)sb);
-      mutate_row_full<NT>(x, s_geo, s_ginfo, sgl, sgu, V, i, rng, gen, a.eta, lane);
+      mutate_row_full<NT>(x, s_geo, s_ginfo, s_cmap, sgl, sgu, p.Vr, i, rng, gen, a.eta, lane);
     } else if (a.mode == 1) {  // apply the row's cached mutations
       apply_row_mutations<NT>(x, rdl(mut_v, k) & 7, mpos, mval, k, lane);
     }
@@ -407,7 +417,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     const Rng rng2(seed2, state_stream(a.stream_key, a.state_keys, a.key0, b));
     const double* gl = a.s.gl + (size_t)b * V;
     const double* gu = a.s.gu + (size_t)b * V;
-    const float lq = __log2f(1.0f - 1.0f / (float)V);
+    const int Vr = p.Vr;
+    const float lq = __log2f(1.0f - 1.0f / (float)Vr);
     for (int k = 0; k < nrw; ++k) {
       if (!(rdl(mut_v, k) & 8)) continue;
       const int i = rc.i0 + wave + VARY_W * k;
@@ -416,18 +427,20 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       int pos = -1;
       for (int j = 0;; ++j) {
         const u32x4 w = rng2.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-        pos += 1 + geo_gap(s_geo, V, w.x, lq);
-        if (pos >= V) break;
+        pos += 1 + geo_gap(s_geo, Vr, w.x, lq);
+        if (pos >= Vr) break;
+        const int cp = s_cmap[pos];  // stored gene (-1: fixed, its mutation is the identity)
+        if (cp < 0) continue;
         double xv = 0.0;
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          if (pos == lane + 64 * t) xv = x[t];
-        if ((pos & 63) == lane) {
-          xv = mutate_gene(xv, gl[MV_IDX(pos, V, CK_AT_BOUNDS)], gu[MV_IDX(pos, V, CK_AT_BOUNDS)],
-                         (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), a.eta);
+          if (cp == lane + 64 * t) xv = x[t];
+        if ((cp & 63) == lane) {
+          xv = mutate_gene(xv, gl[MV_IDX(cp, V, CK_AT_BOUNDS)], gu[MV_IDX(cp, V, CK_AT_BOUNDS)],
+                         (s_ginfo[cp] & 3) == 0, u53(w.y, w.z), a.eta);
 #pragma unroll
           for (int t = 0; t < NT; ++t)
-            if (pos == lane + 64 * t) x[t] = xv;
+            if (cp == lane + 64 * t) x[t] = xv;
         }
       }
       finish_row(k, x);
@@ -1793,7 +1806,8 @@ static hipError_t cons_go(dim3 grid, size_t lds, hipStream_t s, int slot, int h0
 // kernels).  MV_NARROW=0 turns it off (A/B runs).
 static bool use_narrow(const RowsArgs& a) {
   const char* s = std::getenv("MV_NARROW");  // read per launch: tests flip it in-process
-  return !(s && s[0] == '0') && a.do_eval && narrow_ok(a.p) && !(a.mode == 1 && a.cx_kind == 1);
+  return !(s && s[0] == '0') && a.do_eval && narrow_ok(a.p) && !(a.mode == 1 && a.cx_kind == 1) &&
+         !a.p.compact;  // the compact layout runs on the wave-per-row kernels only
 }
 
 template <int NV, bool FULL>

@@ -27,7 +27,8 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
 // workgroup stages the regions it needs with 16-B-per-lane global_load_lds copies.
 //   problem blob  A: constraint program (opa, opk, opc, ocol, pool)       -> k_cons
 //                 B: mutation gap table, gene table, mutable features,
-//                    one-hot group offsets / features                     -> k_gen
+//                    one-hot group offsets / features, cmap [Vr] (gene -> stored gene or
+//                    -1, fixed) and fidx [V] (stored gene -> gene)        -> k_gen
 //                 C: ML scaler at the mutable features (mlS, mlM)         -> k_gen
 //                 S: the slim program of k_genc's phase 2 (DIFF / RATIO_SAFE lane ops and
 //                    ABS_SUMDIFF only): k (fp64), col, pool, sum-diff args -> LDS; the
@@ -36,7 +37,7 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
 //                 E: encoder MinMax at the mutable features (es, em, x0)  -> k_gen
 struct VaryOff {
   unsigned opa, opk, opc, ocol, pool, a_end;      // region A at 0
-  unsigned geo, ginfo, mutf, ooff, ofeat, b_at, b_end;  // region B at b_at
+  unsigned geo, ginfo, mutf, ooff, ofeat, cmap, fidx, b_at, b_end;  // region B at b_at
   unsigned mlS, mlM, c_at, c_end;                 // region C at c_at
   unsigned s_k, s_col, s_pool, s_sd, s_at, s_end;  // region S (staged part) at s_at
   unsigned s_opw, vb;                             // S packed op words; vb = blob bytes
@@ -62,11 +63,13 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   o.a_end = kb(off);
   o.b_at = o.a_end;
   off = o.b_at;
-  o.geo = take((size_t)(p.V + 1) * 4);
+  o.geo = take((size_t)(p.Vr + 1) * 4);
   o.ginfo = take((size_t)((p.V + 3) & ~3) * 4);
   o.mutf = take(Dm4 * 4);
   o.ooff = take((size_t)(p.n_ohe + 1) * 4);
   o.ofeat = take((size_t)(p.n_ohe_feat > 0 ? p.n_ohe_feat : 1) * 4);
+  o.cmap = take((size_t)p.Vr * 4);
+  o.fidx = take((size_t)p.V * 4);
   o.b_end = kb(off);
   o.c_at = o.b_end;
   off = o.c_at;
@@ -193,7 +196,10 @@ hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* gen
 hipError_t launch_obj_mlscale(long total, int D, const double* x, const double* s,
                               const double* m, double* out, hipStream_t stream);
 hipError_t launch_objectives(const ObjArgs& a, hipStream_t stream);
-hipError_t launch_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
+// pool rows (V stored genes) -> population genes [B][P][Vr]: a fixed gene (cmap < 0, compact
+// layout) is its state's bound glr[b][g] (the full layout's genetic lower bound)
+hipError_t launch_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap,
+                             const double* glr, const int* pop_slot, const double* pool,
                              const double* poolF, double* genes, double* F, hipStream_t stream);
 
 }  // namespace mv

@@ -365,7 +365,8 @@ constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream 
 template <int NT>
 __device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double* gown,
                                         const double* goth, const double* gl, const double* gu,
-                                        int V, int m, int side, int on0, int on1, const Rng& rng,
+                                        int V, const int* fidx, int m, int side, int on0, int on1,
+                                        const Rng& rng,
                                         int gen, double eta, int lane, int* sdesc,
                                         double* sres) {
   int slot[NT];
@@ -378,7 +379,7 @@ __device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double
       const bool real = (ginf[t] & 3) == 0;
       if (real ? on0 : on1) {
         const double own = x[t], oth = goth[g];
-        const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
+        const u32x4 w = rng.draw((uint32_t)(m * MUT_J + fidx[g]), (uint32_t)gen, TAG_SBX);
         need = !(w.x & 1u) && fabs(own - oth) > 1.0e-14;
       }
     }
@@ -397,7 +398,7 @@ __device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double
       const bool real = (d >> 16) != 0;
       const double own = gown[g], oth = goth[g];
       const double p0 = side == 0 ? own : oth, p1 = side == 0 ? oth : own;
-      const u32x4 w = rng.draw((uint32_t)(m * MUT_J + g), (uint32_t)gen, TAG_SBX);
+      const u32x4 w = rng.draw((uint32_t)(m * MUT_J + fidx[g]), (uint32_t)gen, TAG_SBX);
       const double lo = gl[g], hi = gu[g];
       double c = sbx_child(p0, p1, real ? lo : lo - INT_WIDEN, real ? hi : hi + INT_WIDEN,
                            u53(w.y, w.z), (w.x & 2u) != 0u, side, eta);
@@ -414,29 +415,31 @@ __device__ __forceinline__ void sbx_row(double* x, const int* ginf, const double
     if (slot[t] >= 0) x[t] = sres[slot[t]];
 }
 
-// Every mutation of row i (the whole geometric-gap draw sequence of mutation_draws, no
-// register cache): the SBX rows take this path since their crossed values exist only in the
-// row loop.
+// Every mutation of row i (the whole geometric-gap draw sequence of mutation_draws over the
+// Vr genes, no register cache): the SBX rows take this path since their crossed values exist
+// only in the row loop.  Positions map to stored genes through cmap (-1: a fixed gene of the
+// compact layout, whose mutation is the identity).
 template <int NT>
 __device__ __forceinline__ void mutate_row_full(double* x, const uint32_t* s_geo,
-                                                const int* s_ginfo, const double* gl,
-                                                const double* gu, int V, int i, const Rng& rng,
-                                                int gen, double eta, int lane) {
-  const float lq = __log2f(1.0f - 1.0f / (float)V);
+                                                const int* s_ginfo, const int* s_cmap,
+                                                const double* gl, const double* gu, int Vr, int i,
+                                                const Rng& rng, int gen, double eta, int lane) {
+  const float lq = __log2f(1.0f - 1.0f / (float)Vr);
   int pos = -1;
   for (int j = 0;; ++j) {
     const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-    pos += 1 + geo_gap(s_geo, V, w.x, lq);
-    if (pos >= V) break;
-    if ((pos & 63) == lane) {
+    pos += 1 + geo_gap(s_geo, Vr, w.x, lq);
+    if (pos >= Vr) break;
+    const int cp = s_cmap[pos];
+    if (cp >= 0 && (cp & 63) == lane) {
       double xv = 0.0;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (pos == lane + 64 * t) xv = x[t];
-      xv = mutate_gene(xv, gl[pos], gu[pos], (s_ginfo[pos] & 3) == 0, u53(w.y, w.z), eta);
+        if (cp == lane + 64 * t) xv = x[t];
+      xv = mutate_gene(xv, gl[cp], gu[cp], (s_ginfo[cp] & 3) == 0, u53(w.y, w.z), eta);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (pos == lane + 64 * t) x[t] = xv;
+        if (cp == lane + 64 * t) x[t] = xv;
     }
   }
 }
@@ -700,8 +703,9 @@ __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, const i
                                                     const double (&mval)[CAP], int k, int lane) {
 #pragma unroll
   for (int q = 0; q < CAP; ++q) {
-    if (q < nmut) {
-      const int pos = MV_IDX(rdl(mpos[q], k), 64 * NT, CK_GEN_APPLY);
+    const int pr = rdl(mpos[q], k);  // stored gene; -1: a fixed gene (compact layout), no-op
+    if (q < nmut && pr >= 0) {
+      const int pos = MV_IDX(pr, 64 * NT, CK_GEN_APPLY);
       const double y = rdl_d(mval[q], k);
       const int tt = pos >> 6;
       const bool me = lane == (pos & 63);

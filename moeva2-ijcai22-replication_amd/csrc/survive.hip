@@ -49,14 +49,18 @@ __global__ void k_init_pool(int B, int P, int O, int V, int S, const double* gen
   }
 }
 
-__global__ void k_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
-                             const double* poolF, double* genes, double* F) {
+__global__ void k_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap, const double* glr,
+                             const int* pop_slot, const double* pool, const double* poolF,
+                             double* genes, double* F) {
   const size_t tot = (size_t)B * P;
   for (size_t t = blockIdx.x; t < tot; t += gridDim.x) {
     const size_t b = t / P;
     const int s = pop_slot[t];
     if (genes)
-      for (int g = threadIdx.x; g < V; g += blockDim.x) genes[t * V + g] = pool[(b * S + s) * V + g];
+      for (int g = threadIdx.x; g < Vr; g += blockDim.x) {
+        const int c = cmap ? cmap[g] : g;
+        genes[t * Vr + g] = c >= 0 ? pool[(b * S + s) * V + c] : glr[b * Vr + g];
+      }
     if (F && threadIdx.x < 3) F[t * 3 + threadIdx.x] = poolF[(b * S + s) * 3 + threadIdx.x];
   }
 }
@@ -122,10 +126,11 @@ hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* gen
   return hipGetLastError();
 }
 
-hipError_t launch_gather_pop(int B, int P, int V, int S, const int* pop_slot, const double* pool,
+hipError_t launch_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap,
+                             const double* glr, const int* pop_slot, const double* pool,
                              const double* poolF, double* genes, double* F, hipStream_t stream) {
-  hipLaunchKernelGGL(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, S, pop_slot, pool,
-                     poolF, genes, F);
+  hipLaunchKernelGGL(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, Vr, S, cmap, glr,
+                     pop_slot, pool, poolF, genes, F);
   return hipGetLastError();
 }
 

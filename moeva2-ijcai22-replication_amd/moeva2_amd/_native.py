@@ -30,7 +30,7 @@ EXPORTED = [
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
     "mv_objcalc_score", "mv_det_pow", "mv_debug_checks", "mv_set_state_streams",
-    "mv_debug_survival_dump",
+    "mv_debug_survival_dump", "mv_get_stored_genes",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -118,6 +118,7 @@ def lib():
             "mv_debug_checks": [_i32p, _i32p],
             "mv_set_state_streams": [vp, C.c_int32, C.c_int64],
             "mv_debug_survival_dump": [_f64p],
+            "mv_get_stored_genes": [vp, _i32p, _i32p],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -349,6 +350,15 @@ class Engine:
         state b draws from Philox stream first_state + b, its GLOBAL index."""
         check(lib().mv_set_state_streams(self._h, 1 if enabled else 0, int(first_state)))
         self.state_streams = (bool(enabled), int(first_state))
+
+    def stored_genes(self) -> np.ndarray:
+        """The attack's gene layout for the bound states (mv_get_stored_genes): bool [V],
+        False for a gene no attack on these states can change (integer, xl == xu == its
+        initial value in every state), which the attack does not store or sum."""
+        st = np.zeros(self.prog.V, np.int32)
+        n = C.c_int32(0)
+        check(lib().mv_get_stored_genes(self._h, st.ctypes.data_as(_i32p), C.byref(n)))
+        return st.astype(bool)
 
     def set_mlp_precision(self, dtype: str = "fp32"):
         """Classifier precision of the fitness path: "fp32" (parity default) or "bf16" (perf

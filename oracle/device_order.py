@@ -30,6 +30,12 @@ and the device attack can be compared trajectory for trajectory:
 Every element value (each constraint column, each scaled feature) is the oracle's own; only
 the order of the sums is the engine's.
 
+* ``fixed`` (bool [D], optional): the attack's compact gene layout (mv_get_stored_genes,
+  csrc/api.cpp stored_genes): mutable features whose gene never changes on the bound state
+  set.  The attack evaluates them as immutable features -- folded into the layer-1 bias in
+  feature order, left out of the classifier's k sequence and of f2's lanes -- so its f1 /
+  f2 are these functions with ``fixed`` set.
+
 * pow in the variation operators: ``det_pow`` restates csrc/detmath.h operation for
   operation (np.power and the device library's pow each round within about an ulp but
   not identically; run_attack(..., pow_fn=det_pow) gives the engine's mutated genes).
@@ -187,7 +193,31 @@ def _dense_mfma(h, W, K):
     return acc
 
 
-def layer0_bias(prob: "mo.Problem"):
+def _mutable(prob, fixed):
+    """The engine's mutable features: the layout's, less the compact layout's fixed ones."""
+    m = np.asarray(prob.lay.mutable_mask, bool)
+    return m if fixed is None else m & ~np.asarray(fixed, bool)
+
+
+def compact_fixed(lay, probs):
+    """The attack's compact layout for a state set (csrc/api.cpp stored_genes): the feature
+    mask of the mutable features whose gene is an integer gene with xl == xu == its initial
+    value in every state (``probs``: the states' problems).  One-hot layouts are never
+    compacted; nor is a layout whose genes would all be fixed."""
+    fixed = np.zeros(lay.D, bool)
+    if lay.ohe_masks:
+        return fixed
+    g_fixed = mo.genetic_types(lay) == "int"
+    for prob in probs:
+        gl, gu = mo.genetic_bounds(lay, prob.xl, prob.xu)
+        g0 = mo.ml_to_genetic(lay, prob.x_init[None, :])[0]
+        g_fixed &= (gl == gu) & (g0 == gl) & (np.rint(g0) == g0)
+    if not g_fixed.all():
+        fixed[np.where(lay.mutable_mask)[0][g_fixed]] = True
+    return fixed
+
+
+def layer0_bias(prob: "mo.Problem", fixed=None):
     """k_setup_states: b1 + fmaf chain over the immutable features (ascending) of the
     ML-scaled initial state."""
     W0 = prob.weights[0].astype(np.float32)
@@ -196,13 +226,13 @@ def layer0_bias(prob: "mo.Problem"):
         x = mo.minmax_transform(x[None, :], prob.ml_scale, prob.ml_min)[0]
     x32 = x.astype(np.float32)
     s = np.zeros(W0.shape[1], np.float32)
-    for f in np.where(~prob.lay.mutable_mask)[0]:
+    for f in np.where(~_mutable(prob, fixed))[0]:
         s = _fma32(x32[f], W0[f], s)
     return (prob.biases[0].astype(np.float32) + s).astype(np.float32)
 
 
-def f1_device_order(prob: "mo.Problem", x_f: np.ndarray) -> np.ndarray:
-    mut = np.where(prob.lay.mutable_mask)[0]
+def f1_device_order(prob: "mo.Problem", x_f: np.ndarray, fixed=None) -> np.ndarray:
+    mut = np.where(_mutable(prob, fixed))[0]
     x_ml = x_f if prob.ml_scale is None else mo.minmax_transform(x_f, prob.ml_scale, prob.ml_min)
     Dm = mut.size
     K0 = (Dm + 15) // 16 * 16
@@ -211,7 +241,7 @@ def f1_device_order(prob: "mo.Problem", x_f: np.ndarray) -> np.ndarray:
     W0 = np.zeros((K0, prob.weights[0].shape[1]), np.float32)
     W0[:Dm] = prob.weights[0][mut].astype(np.float32)
     nl = len(prob.weights)
-    h = np.maximum(_dense_mfma(h, W0, K0) + layer0_bias(prob), np.float32(0))
+    h = np.maximum(_dense_mfma(h, W0, K0) + layer0_bias(prob, fixed), np.float32(0))
     for l in range(1, nl - 1):
         W = prob.weights[l].astype(np.float32)
         h = np.maximum(_dense_mfma(h, W, W.shape[0]) + prob.biases[l].astype(np.float32),
@@ -262,8 +292,8 @@ def lane_partials(terms):
     return acc
 
 
-def f2_device_order(prob: "mo.Problem", x_f: np.ndarray) -> np.ndarray:
-    mut = np.where(prob.lay.mutable_mask)[0]
+def f2_device_order(prob: "mo.Problem", x_f: np.ndarray, fixed=None) -> np.ndarray:
+    mut = np.where(_mutable(prob, fixed))[0]
     d = mo.minmax_transform(x_f, prob.enc_scale, prob.enc_min)[:, mut] - prob.x_init_mm[mut]
     if prob.norm in ("inf", np.inf):
         f2 = np.abs(d).max(axis=1)
@@ -294,11 +324,13 @@ def f3_device_order(G: np.ndarray, op_codes) -> np.ndarray:
     return f3 + sd
 
 
-def evaluate_device_order(prob: "mo.Problem", genes: np.ndarray, op_codes, return_g=False):
-    """``moeva_oracle.evaluate`` with the engine's summation orders (module docstring)."""
+def evaluate_device_order(prob: "mo.Problem", genes: np.ndarray, op_codes, return_g=False,
+                          fixed=None):
+    """``moeva_oracle.evaluate`` with the engine's summation orders (module docstring);
+    ``fixed``: the attack's compact layout (features evaluated as immutable)."""
     x_f = mo.genetic_to_ml(prob.lay, genes, prob.x_init)
     g = prob.constraints_fn(x_f)
     g = g * (g > 0).astype(np.float64)
-    F = np.column_stack([f1_device_order(prob, x_f), f2_device_order(prob, x_f),
+    F = np.column_stack([f1_device_order(prob, x_f, fixed), f2_device_order(prob, x_f, fixed),
                          f3_device_order(g, op_codes)])
     return (F, g) if return_g else F

@@ -15,7 +15,9 @@ sums in the order the HIP kernels use) and the variation operators use the engin
 (oracle/device_order.py:det_pow = csrc/detmath.h), so the oracle's attack and the device
 attack follow the same trajectories unless a rare fp32 double rounding flips a comparison.
 The classifier's softmax is Keras's fp32 arithmetic on both sides (csrc/rowops.h softmax_e,
-device_order.softmax_keras32).  The success rates of the numpy-order oracle
+device_order.softmax_keras32).  The attack's compact gene layout (device_order.compact_fixed
+over the configuration's states: botnet's 120 fixed integer genes) is part of the engine's
+order: those features are evaluated as immutable.  The success rates of the numpy-order oracle
 (moeva_oracle.evaluate) at the same seed are kept in the fixture as
 ``success_rate_numpy_order`` (NUMPY_ORDER below).
 
@@ -44,6 +46,7 @@ CONFIGS = {
 
 _P = None
 _CODES = None
+_FIXED = None
 
 # success rates o1..o7 of the same configurations with numpy's summation orders (the first
 # version of these fixtures; one seed, so they carry the attack's seed-to-seed spread)
@@ -54,12 +57,13 @@ NUMPY_ORDER = {
 }
 
 
-def _init(project):
+def _init(project, B):
     os.environ["OMP_NUM_THREADS"] = "1"
     from threadpoolctl import threadpool_limits
 
     threadpool_limits(1)
-    global _P, _CODES
+    global _P, _CODES, _FIXED
+    from oracle import device_order as do
     from oracle.problems import PROJECTS, Project
 
     from moeva2_amd.experiments.united.utils import STR_TO_CONSTRAINTS_CLASS
@@ -70,6 +74,7 @@ def _init(project):
     feat = os.path.join(res, PROJECTS[project][0])
     c = STR_TO_CONSTRAINTS_CLASS[project](feat, feat.replace("features", "constraints"))
     _CODES = build_device_program(c).op_code
+    _FIXED = do.compact_fixed(_P.lay, [_P.problem(x, norm=2) for x in _P.x[:B]])
 
 
 def digest(X: np.ndarray) -> int:
@@ -91,7 +96,7 @@ def one_state(args):
     ref = energy_ref_dirs(3, n_pop, seed=1)
 
     def ev(prob, genes, return_g=False):
-        return do.evaluate_device_order(prob, genes, _CODES, return_g)
+        return do.evaluate_device_order(prob, genes, _CODES, return_g, fixed=_FIXED)
 
     r = mo.run_attack(p.problem(p.x[b], norm=2), ref, n_gen, n_pop + 3, n_off, seed,
                       evaluate_fn=ev, pow_fn=do.det_pow)
@@ -100,7 +105,7 @@ def one_state(args):
     obj = mo.objectives_calc(p.x[b], x_f, p.constraints, p.types, sc, mn, p.weights, p.biases,
                              1, sc, mn, 2)
     resp = mo.objectives_respected(obj, thr, eps).any(axis=0)
-    return b, resp, float(obj[:, 1].min()), digest(r.pop_X)
+    return b, resp, float(obj[:, 1].min()), digest(r.pop_X), int(_FIXED.sum())
 
 
 def main(name, procs=None):
@@ -111,8 +116,9 @@ def main(name, procs=None):
     best = np.zeros(B)
     dig = np.zeros(B, np.int64)
     jobs = [(b, n_gen, n_pop, n_off, seed, eps, thr) for b in range(B)]
-    with get_context("spawn").Pool(procs, initializer=_init, initargs=(project,)) as pool:
-        for k, (b, r, f1, d) in enumerate(pool.imap_unordered(one_state, jobs)):
+    n_fixed = 0
+    with get_context("spawn").Pool(procs, initializer=_init, initargs=(project, B)) as pool:
+        for k, (b, r, f1, d, n_fixed) in enumerate(pool.imap_unordered(one_state, jobs)):
             resp[b], best[b], dig[b] = r, f1, d
             if (k + 1) % max(1, B // 20) == 0:
                 print(f"{name}: {k + 1}/{B} states, {time.time() - t0:.0f} s", flush=True)
@@ -122,6 +128,7 @@ def main(name, procs=None):
                         best_f1=best, pop_digest=dig, success_rate=resp.mean(axis=0),
                         success_rate_numpy_order=np.asarray(NUMPY_ORDER[name]),
                         evaluation_order="engine (oracle/device_order.py)",
+                        compact_fixed_features=n_fixed,
                         variation_pow="det_pow (oracle/device_order.py = csrc/detmath.h)",
                         cpu_seconds=time.time() - t0, procs=procs)
     print(name, "success rates o1..o7", resp.mean(axis=0), f"{time.time() - t0:.0f} s")

@@ -200,9 +200,15 @@ def test_wide_mlp_config_matches_fp32_reference():
         outs.append((g.cpu().numpy(), Fa.cpu().numpy()))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    # the attack ran the compact gene layout (120 fixed botnet genes evaluated as immutable
+    # features), mv_evaluate the full one: same values, f1 / f2 summed in another order
+    assert (~eng.stored_genes()).sum() == 120
     Fe = torch.empty((X.shape[0], 23, 3), dtype=torch.float64, device="cuda")
     eng.evaluate(torch.as_tensor(outs[0][0], device="cuda"), Fe)
-    np.testing.assert_array_equal(Fe.cpu().numpy(), outs[0][1])
+    Fe = Fe.cpu().numpy()
+    np.testing.assert_allclose(Fe[..., 0], outs[0][1][..., 0], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(Fe[..., 1], outs[0][1][..., 1], rtol=1e-12, atol=1e-15)
+    np.testing.assert_array_equal(Fe[..., 2], outs[0][1][..., 2])
 
 
 # ------------------------------------------------------------------ bf16 perf mode
@@ -628,6 +634,70 @@ def test_slim_program_matches_full(monkeypatch, name, B, P, O, G, hist, cx):
     np.testing.assert_array_equal(F1.cpu().numpy(), F0.cpu().numpy())
     if hist:
         np.testing.assert_array_equal(h1.cpu().numpy(), h0.cpu().numpy())
+
+
+def _fixed_features(p, stored):
+    """Feature mask of the genes the attack's compact layout does not store (IDENT problems:
+    gene g is mutable feature g)."""
+    fixed = np.zeros(p.lay.mutable_mask.shape[0], bool)
+    fixed[np.where(p.lay.mutable_mask)[0][~stored]] = True
+    return fixed
+
+
+@pytest.mark.parametrize("name,cx", [("botnet", "two_point"), ("botnet", "sbx"),
+                                     ("botnet_augmented", "two_point")])
+def test_compact_layout_attack_objectives_bit_exact(name, cx):
+    """The attack's compact gene layout (mv_get_stored_genes): on the shipped botnet states
+    the 120 integer genes with xl == xu == x_init are not stored.  The final population's
+    fixed genes are their bounds, and its F is bit-identical to the oracle's objectives in
+    the engine's order with those features evaluated as immutable (device_order ``fixed``)."""
+    from oracle import device_order as do
+    from moeva2_amd.problem import build_device_program
+
+    p = Project(name)
+    c = make_constraints(name)
+    codes = build_device_program(c).op_code
+    X = p.x[:5]
+    eng, g, F, _, _ = _attack(name, X, 5, 41, P=43, O=20, crossover=cx)
+    stored = eng.stored_genes()
+    assert (~stored).sum() == 120, (~stored).sum()
+    fixed = _fixed_features(p, stored)
+    genes, F = g.cpu().numpy(), F.cpu().numpy()
+    for b in range(X.shape[0]):
+        prob = p.problem(X[b])
+        gl, gu = mo.genetic_bounds(p.lay, prob.xl, prob.xu)
+        np.testing.assert_array_equal(genes[b][:, ~stored], np.broadcast_to(gl[~stored],
+                                                                            genes[b][:, ~stored].shape))
+        ref = do.evaluate_device_order(prob, genes[b], codes, fixed=fixed)
+        np.testing.assert_array_equal(F[b], ref)
+
+
+@pytest.mark.parametrize("cx", ["two_point", "sbx"])
+def test_compact_layout_tracks_full_layout(monkeypatch, cx):
+    """MV_COMPACT=0 stores every gene.  Both layouts consume the same draws over all 432
+    genes, so the populations are the same ones up to the last-bit differences of f1 / f2
+    (the compact layout leaves the fixed features' zero distance terms out and folds their
+    constant classifier terms into the bias): most states end bit-identical, and the
+    compact run's F agrees with the full layout's re-evaluation of its own genes."""
+    p = Project("botnet")
+    X = p.x[:8]
+    monkeypatch.setenv("MV_COMPACT", "0")
+    e0, g0, F0, _, _ = _attack("botnet", X, 6, 43, P=43, O=20, crossover=cx)
+    assert e0.stored_genes().all()
+    monkeypatch.setenv("MV_COMPACT", "1")
+    e1, g1, F1, _, _ = _attack("botnet", X, 6, 43, P=43, O=20, crossover=cx)
+    assert (~e1.stored_genes()).sum() == 120
+    g0, g1n = g0.cpu().numpy(), g1.cpu().numpy()
+    same = sum(np.array_equal(g0[b], g1n[b]) for b in range(X.shape[0]))
+    print(cx, "bit-identical final populations", same, "/", X.shape[0])
+    assert same >= X.shape[0] // 2
+    F2 = torch.empty_like(F1)
+    e1.evaluate(g1, F2)  # the full layout (every gene) on the compact run's genes
+    torch.cuda.synchronize()
+    F1n, F2n = F1.cpu().numpy(), F2.cpu().numpy()
+    np.testing.assert_allclose(F1n[..., 0], F2n[..., 0], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(F1n[..., 1], F2n[..., 1], rtol=1e-12, atol=1e-15)
+    np.testing.assert_array_equal(F1n[..., 2], F2n[..., 2])
 
 
 def test_attack_invariants_lcld():
