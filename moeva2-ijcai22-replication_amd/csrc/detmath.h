@@ -15,6 +15,14 @@
 // binary powering in double-double.  Measured against np.power (tests/test_detpow_cpu.py):
 // at most 1 ulp apart on the operators' argument ranges.  Identity with the oracle is the
 // point, not the last bit of np.power.
+//
+// det_pow<true> (the device's variation operators) takes each exact product from an FMA,
+// p = a b, e = fma(a, b, -p), where Dekker's split-based product is exact too: both then
+// return the one representable error a b - p, so the result is bit-identical to det_pow<>
+// (and to the oracle) at a fraction of the operations.  Dekker is exact unless a partial
+// product underflows: y ln x (|y| >= 2^-10, |ln x| >= 2^-53 for x != 1) and the reciprocal
+// correction (q rh ~ 1) never do; the binary powering's products do only for x < 1, so
+// there the split is kept.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,15 +46,25 @@ __host__ __device__ inline void det_two_sum(double a, double b, double& s, doubl
   const double bb = s - a;
   e = (a - (s - bb)) + (b - bb);
 }
+template <bool FMA>
+__host__ __device__ inline void det_two_prod_x(double a, double b, double& p, double& e) {
+  if (FMA) {
+    p = a * b;
+    e = fma(a, b, -p);
+  } else {
+    det_two_prod(a, b, p, e);
+  }
+}
 __host__ __device__ inline void det_fast_two_sum(double a, double b, double& s, double& e) {
   s = a + b;
   e = b - (s - a);
 }
 // double-double product (hi, lo normalised)
+template <bool FMA = false>
 __host__ __device__ inline void det_dd_mul(double ah, double al, double bh, double bl, double& h,
                                            double& l) {
   double p, e;
-  det_two_prod(ah, bh, p, e);
+  det_two_prod_x<FMA>(ah, bh, p, e);
   e = e + (ah * bl + al * bh);
   det_fast_two_sum(p, e, h, l);
 }
@@ -100,6 +118,7 @@ __host__ __device__ inline double det_exp2(double th, double tl) {
   return ldexp(y, (int)kd);
 }
 
+template <bool FMA = false>
 __host__ __device__ inline double det_pow(double x, double y) {
   if (x != x || y != y) return x + y;  // NaN
   if (y == 0.0 || x == 1.0) return 1.0;
@@ -121,21 +140,29 @@ __host__ __device__ inline double det_pow(double x, double y) {
       return y < 0.0 ? 1.0 / r : r;
     }
     double rh = 1.0, rl = 0.0, bh = x, bl = 0.0;  // double-double
-    while (n) {
-      if (n & 1) det_dd_mul(rh, rl, bh, bl, rh, rl);
-      n >>= 1;
-      if (n) det_dd_mul(bh, bl, bh, bl, bh, bl);
+    if (FMA && x >= 1.0) {  // every product >= 1: no partial product underflows
+      while (n) {
+        if (n & 1) det_dd_mul<true>(rh, rl, bh, bl, rh, rl);
+        n >>= 1;
+        if (n) det_dd_mul<true>(bh, bl, bh, bl, bh, bl);
+      }
+    } else {
+      while (n) {
+        if (n & 1) det_dd_mul(rh, rl, bh, bl, rh, rl);
+        n >>= 1;
+        if (n) det_dd_mul(bh, bl, bh, bl, bh, bl);
+      }
     }
     if (y > 0.0) return rh;
     const double q = 1.0 / rh;  // 1 / (rh + rl), one correction step
     double p, pe;
-    det_two_prod(q, rh, p, pe);
+    det_two_prod_x<FMA>(q, rh, p, pe);
     const double rem = ((1.0 - p) - pe) - q * rl;
     return q + rem / rh;
   }
   double lh, ll, th, tl0;
   det_log2(x, lh, ll);
-  det_two_prod(y, lh, th, tl0);
+  det_two_prod_x<FMA>(y, lh, th, tl0);
   double tl = tl0 + y * ll;
   det_fast_two_sum(th, tl, th, tl);
   return det_exp2(th, tl);

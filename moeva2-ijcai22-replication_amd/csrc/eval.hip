@@ -626,16 +626,19 @@ __global__ __launch_bounds__(CONS_T) void k_cons(int slot, int hist_row0, int ro
 // instances up to 8 genes per lane spill a few registers to scratch) for a 4th resident
 // workgroup per CU -- with the slim phase-2 LDS (~37 KiB) four fit.  Round 4 A/B on the
 // botnet headline: 172.2 vs 161.5 M evals/s (k_genc 119.5 vs 137.6 us, one state group).
-// The SBX and 16-genes-per-lane instances keep the allocator's choice (their register needs
-// would spill heavily).  MV_GENC_WAVES (development builds) overrides the 4.
+// SBX instances: 4 waves up to 5 genes per lane (botnet's compact layout: 140 -> 128
+// VGPRs, 6 spilled; SBX option 124.0 -> 133.1 M evals/s, A/B on one box), the allocator's
+// choice above that, like the 16-genes-per-lane instances (their register needs would spill
+// heavily).  MV_GENC_WAVES / MV_GENC_SBX_WAVES (development builds) override the 4 / 1.
 #ifndef MV_GENC_WAVES
 #define MV_GENC_WAVES 4
 #endif
 #ifndef MV_GENC_SBX_WAVES
 #define MV_GENC_SBX_WAVES 1
 #endif
-#define MV_GENC_BOUNDS \
-  __launch_bounds__(VARY_T, NT > 8 ? 1 : (SBX ? MV_GENC_SBX_WAVES : MV_GENC_WAVES))
+#define MV_GENC_BOUNDS                                                                  \
+  __launch_bounds__(VARY_T, NT > 8 ? 1                                                 \
+                                   : (SBX ? (NT <= 5 ? 4 : MV_GENC_SBX_WAVES) : MV_GENC_WAVES))
 template <bool IDENT, int NT, bool SBX, bool SLIM>
 __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows_wg) {
   static_assert(VARY_T == CONS_T, "k_genc runs both phases on the same waves");

@@ -223,7 +223,7 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
 }
 
 // pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction,
-// det_pow (detmath.h) for np.power.
+// det_pow (detmath.h; its bit-identical FMA-product form) for np.power.
 __device__ __forceinline__ double poly_mut(double x, double xl, double xu, double u, double eta) {
   const double d1 = (x - xl) / (xu - xl);
   const double d2 = (xu - x) / (xu - xl);
@@ -231,12 +231,12 @@ __device__ __forceinline__ double poly_mut(double x, double xl, double xu, doubl
   double dq;
   if (u <= 0.5) {
     const double xy = 1.0 - d1;
-    const double val = 2.0 * u + (1.0 - 2.0 * u) * det_pow(xy, eta + 1.0);
-    dq = det_pow(val, mp) - 1.0;
+    const double val = 2.0 * u + (1.0 - 2.0 * u) * det_pow<true>(xy, eta + 1.0);
+    dq = det_pow<true>(val, mp) - 1.0;
   } else {
     const double xy = 1.0 - d2;
-    const double val = 2.0 * (1.0 - u) + 2.0 * (u - 0.5) * det_pow(xy, eta + 1.0);
-    dq = 1.0 - det_pow(val, mp);
+    const double val = 2.0 * (1.0 - u) + 2.0 * (u - 0.5) * det_pow<true>(xy, eta + 1.0);
+    dq = 1.0 - det_pow<true>(val, mp);
   }
   double y = x + dq * (xu - xl);
   if (y < xl) y = xl;
@@ -323,10 +323,11 @@ __device__ __forceinline__ double sbx_child(double p0, double p1, double xl, dou
   // c[0] takes c1 (lower side) unless swapped; c[1] the other one
   const bool low = (side == 0) != swap;
   const double beta = low ? 1.0 + (2.0 * (y1 - xl) / delta) : 1.0 + (2.0 * (xu - y2) / delta);
-  const double alpha = 2.0 - det_pow(beta, -(eta + 1.0));
+  const double alpha = 2.0 - det_pow<true>(beta, -(eta + 1.0));
   const double ex = 1.0 / (eta + 1.0);
   const double betaq =
-      rand <= (1.0 / alpha) ? det_pow((rand * alpha), ex) : det_pow((1.0 / (2.0 - rand * alpha)), ex);
+      rand <= (1.0 / alpha) ? det_pow<true>((rand * alpha), ex)
+                            : det_pow<true>((1.0 / (2.0 - rand * alpha)), ex);
   double c = low ? 0.5 * ((y1 + y2) - betaq * delta) : 0.5 * ((y1 + y2) + betaq * delta);
   if (c < xl) c = xl;  // set_to_bounds_if_outside_by_problem
   if (c > xu) c = xu;

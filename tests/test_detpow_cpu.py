@@ -5,6 +5,8 @@ argument ranges of polynomial mutation (softmax_mutation.py:77-103: x^(eta+1) wi
 u^(1/(eta+1))), plus the special values; and within 1 ulp of np.power (the reference's pow)
 there.  No GPU needed: the host build of detmath.h is the same IEEE operation sequence as
 the device build (tests/test_gpu_parity.py::test_variation_vs_oracle checks the device)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -51,3 +53,24 @@ def test_det_pow_special_values():
         assert np.array_equal(a, b, equal_nan=True), y
     assert det_pow(0.0, 21.0) == 0.0 and np.isnan(det_pow(1.0, np.nan))  # NaN first
     assert det_pow(0.25, 0.5) == 0.5 and det_pow(3.0, 4.0) == 81.0
+
+
+def test_det_pow_fma_products_bit_identical(tmp_path):
+    """The device calls det_pow<true>: exact products from an FMA instead of Dekker's split
+    (csrc/detmath.h).  Built for the host and run on 3 M SBX / mutation arguments, it
+    returns det_pow<>'s bits -- the oracle's -- on every one."""
+    import shutil
+    import subprocess
+
+    cxx = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(cxx):
+        pytest.skip("hipcc not found")
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(os.path.dirname(here), "moeva2-ijcai22-replication_amd", "csrc")
+    exe = str(tmp_path / "detpow_fma_check")
+    subprocess.run([cxx, "-O2", "-ffp-contract=off", "-std=c++17", "-I", csrc,
+                    os.path.join(here, "native", "detpow_fma_check.cpp"), "-o", exe],
+                   check=True, capture_output=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0 and "mismatches 0" in r.stdout, r.stdout
