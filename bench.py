@@ -376,7 +376,10 @@ def main():
     eval_bytes = 2 * V * 8 + 3 * 8
     dims_full = list(eng_dims(eng))
     eval_flops = 2 * sum(a * b for a, b in zip(dims_full[:-1], dims_full[1:]))
-    dims_exec = [Dm] + dims_full[1:]
+    # the attack's compact gene layout (mv_get_stored_genes) evaluates its fixed genes'
+    # features as immutable ones too: layer 0 runs over the stored genes only
+    n_fixed = int((~eng.stored_genes()).sum())
+    dims_exec = [Dm - n_fixed] + dims_full[1:]
     exec_flops = 2 * sum(a * b for a, b in zip(dims_exec[:-1], dims_exec[1:]))
     # per-kernel algorithmic bytes per offspring row:
     #   k_gen : parent genes read + child genes written (2*V*8) + fp32 ML row (Dm4*4) + f2 (8)
@@ -483,6 +486,7 @@ def main():
                    "classifier_dtype": ("bf16 perf mode (bf16 MFMA, fp32 accumulate; not a "
                                         "parity result)" if bf16 else "f32 (MFMA)"),
                    "crossover": args.crossover,
+                   "genes_stored": int(V) - n_fixed,
                    "schedule": "per-phase kernel chain",
                    "parallelism": par},
         "attack_wall_clock_per_1k_states_s": elapsed / args.steps / states_total * 1000.0,
