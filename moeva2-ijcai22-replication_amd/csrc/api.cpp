@@ -347,8 +347,14 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
     }
     put(vo.geo, geo.data(), (size_t)(Vr + 1) * 4);
     {  // region S: k_genc's slim program (kernels.h); the packed words mirror rowops pack_op
+      // with SlotRow operands: slot j < Dm = stored mutable feature j (the wave's row buffer),
+      // Dm + f = feature f of x_init (IDENT problems: k_genc's only ones)
       const int n_lane = C - n_sd;
-      p.slim = n_lane <= 64 * OPS_REG;
+      p.slim = p.ident && n_lane <= 64 * OPS_REG && Dm + D < 0x4000;
+      std::vector<int> slot(D);
+      for (int f = 0; f < D; ++f) slot[f] = Dm + f;
+      for (int j = 0; j < Dm; ++j) slot[mut[j]] = j;
+      auto sl = [&](int f) { return f >= 0 && f < D ? slot[f] : 0; };
       std::vector<double> k1(C);
       std::vector<int> sd((size_t)(n_sd > 0 ? n_sd : 1) * 4, 0);
       std::vector<unsigned> opw(C);
@@ -357,16 +363,21 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
         const int* ar = &sarg[(size_t)k * 4];
         if (k < n_lane) {
           p.slim &= (scode[k] == MV_OP_DIFF || scode[k] == MV_OP_RATIO_SAFE) && ar[0] >= 0 &&
-                    ar[0] < 0x4000 && ar[1] >= 0 && ar[1] < 0x4000;
-          opw[k] = (unsigned)scode[k] | ((unsigned)ar[0] << 4) | ((unsigned)ar[1] << 18);
+                    ar[0] < D && ar[1] >= 0 && ar[1] < D;
+          opw[k] = (unsigned)scode[k] | ((unsigned)sl(ar[0]) << 4) | ((unsigned)sl(ar[1]) << 18);
         } else {
           opw[k] = 0u;
           for (int q = 0; q < 4; ++q) sd[(size_t)(k - n_lane) * 4 + q] = ar[q];
         }
       }
+      std::vector<int> spool(h.n_pool > 0 ? h.n_pool : 1, 0);
+      for (int q = 0; q < h.n_pool; ++q) {
+        p.slim &= h.pool[q] >= 0 && h.pool[q] < D;
+        spool[q] = sl(h.pool[q]);
+      }
       put(vo.s_k, k1.data(), (size_t)C * 8);
       put(vo.s_col, scol.data(), (size_t)C * 4);
-      put(vo.s_pool, h.pool.data(), (size_t)h.n_pool * 4);
+      put(vo.s_pool, spool.data(), (size_t)h.n_pool * 4);
       put(vo.s_sd, sd.data(), sd.size() * 4);
       put(vo.s_opw, opw.data(), (size_t)C * 4);
       if (std::getenv("MV_SLIM") && std::getenv("MV_SLIM")[0] == '0') p.slim = 0;  // A/B

@@ -499,7 +499,8 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   double xa[NT], xb[NT];
   if (nrw > 0) load_row(0, xa);
   if (nrw > 1) load_row(1, xb);
-  // LDS: [program region (A, or S when SLIM)][X: x_init][one row buffer per wave]
+  // LDS: [program region (A, or S when SLIM)][X: x_init][one row buffer per wave: the D
+  // features, or SLIM the Dm stored mutable features (SlotRow)]
   const unsigned pa = SLIM ? o.s_end - o.s_at : o.a_end;
   const int n_lane = p.C - p.n_sumdiff;
   const int kops = min(OPS_REG, (n_lane + 63) >> 6);
@@ -530,11 +531,11 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
-  double* xrow = (double*)(smem + pa + o.x_end + wave * o.rb);
-  {
-    const double* s_xi = (const double*)(smem + pa + o.xi);
+  double* xrow = (double*)(smem + pa + o.x_end + wave * (SLIM ? o.rbs : o.rb));
+  const double* s_xi = (const double*)(smem + pa + o.xi);
+  if (!SLIM)
     for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
-  }
+  const SlotRow srow{xrow, s_xi, p.Dm};
   OpTab tab;
   if (SLIM) {
     tab.code = nullptr;
@@ -570,7 +571,9 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (lane + 64 * t < V) {
-        if (IDENT)
+        if (SLIM)  // IDENT: stored gene c is mutable slot c
+          xrow[lane + 64 * t] = x[t];
+        else if (IDENT)
           xrow[(ginf[t] >> 17) & 0x7FFF] = x[t];
         else
           scatter_gene(p, xrow, ginf[t], x[t]);
@@ -581,8 +584,12 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     double* hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows +
                                       MV_IDX(hist_row0 + i, a.hist_rows, CK_CONS_DST)) * a.hist_w
                           : nullptr;
-    const double f3 = constraints_regs<FULL, SLIM>(tab, opw, kops, xrow, lane, grow,
-                                             (hrow && a.hist_w > 3) ? hrow + 3 : nullptr);
+    double* hc = (hrow && a.hist_w > 3) ? hrow + 3 : nullptr;
+    double f3;
+    if constexpr (SLIM)
+      f3 = constraints_regs<FULL, true>(tab, opw, kops, srow, lane, grow, hc);
+    else
+      f3 = constraints_regs<FULL, false>(tab, opw, kops, (const double*)xrow, lane, grow, hc);
     // The row's destination is read from lane k HERE, with every lane active: a readlane
     // of a lane that is inactive at that point returns an undefined value.  (Round 3 read
     // it inside the lane-0 branch below.  Whenever the compiler spilled dst_v, its reload

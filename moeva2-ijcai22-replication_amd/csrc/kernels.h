@@ -44,6 +44,7 @@ struct VaryOff {
   unsigned xi, x_end;                             // region X at 0
   unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
   unsigned rb;                                    // ML row buffer bytes
+  unsigned rbs;                                   // slim row buffer bytes (Dm doubles)
 };
 __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   VaryOff o{};
@@ -96,6 +97,7 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   o.x0 = take(Dm4 * 8);
   o.sb = kb(off);
   o.rb = (unsigned)(((size_t)p.D * 8 + 15) & ~(size_t)15);
+  o.rbs = (unsigned)(((size_t)p.Dm * 8 + 15) & ~(size_t)15);
   return o;
 }
 // k_gen keeps the ML-scaler / encoder coefficients of its genes in registers for IDENT
@@ -139,9 +141,10 @@ __host__ __device__ inline unsigned gen_lds_sbx(const GenLds& l, int nt) {
 __host__ __device__ inline unsigned cons_lds_total(const VaryOff& o) {
   return o.a_end + o.x_end + CONS_W * o.rb;
 }
-// k_genc's phase 2 with the slim program (DProblem.slim): region S, region X, one row per wave
+// k_genc's phase 2 with the slim program (DProblem.slim): region S, region X, one row of the
+// stored mutable features per wave (the operands are SlotRow slots)
 __host__ __device__ inline unsigned cons_lds_slim(const VaryOff& o) {
-  return (o.s_end - o.s_at) + o.x_end + CONS_W * o.rb;
+  return (o.s_end - o.s_at) + o.x_end + CONS_W * o.rbs;
 }
 
 // k_predict: TR-row tiles (32, or 16 for inputs too wide for a 32-row tile)

@@ -115,10 +115,23 @@ __device__ __forceinline__ double eval_op(const OpTab& t, int c, const XR& x) {
   return __builtin_nan("");
 }
 
+// The slim program's operand view (k_genc phase 2): slot s < dm is stored mutable feature s,
+// held in the wave's row buffer; slot dm + f is feature f of the state's x_init (region X,
+// shared by the waves).  The row buffer is then dm doubles instead of D.
+struct SlotRow {
+  const double* row;
+  const double* xi;
+  int dm;
+  __device__ __forceinline__ double operator[](int s) const {
+    return s < dm ? row[s] : xi[s - dm];
+  }
+};
+
 // |sum(pool[a0:a1]) - sum(pool[a1:a2])| with all 64 lanes, one reduction of the per-lane
 // differences (exact for the integer-valued features of every shipped program; the
 // summation order differs from numpy otherwise).
-__device__ __forceinline__ double sumdiff_wave(const OpTab& t, int c, const double* x, int lane) {
+template <class XR>
+__device__ __forceinline__ double sumdiff_wave(const OpTab& t, int c, const XR& x, int lane) {
   const int4 ar = t.sd ? t.sd[c - t.n_lane] : t.arg[c];
   double s = 0.0;
   for (int q = ar.x + lane; q < ar.y; q += 64) s += x[t.pool[q]];
@@ -165,10 +178,11 @@ __device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
   return (unsigned)t.code[c] | ((unsigned)ar.x << 4) | ((unsigned)ar.y << 18);
 }
 
-// SLIM: every lane op is DIFF / RATIO_SAFE and held in opw (DProblem.slim); k from t.k1.
-template <bool FULL, bool SLIM = false>
+// SLIM: every lane op is DIFF / RATIO_SAFE and held in opw (DProblem.slim); k from t.k1;
+// operands are SlotRow slots.
+template <bool FULL, bool SLIM = false, class XR>
 __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigned* opw, int kops,
-                                                   const double* xrow, int lane, double* grow,
+                                                   const XR& xrow, int lane, double* grow,
                                                    double* hcols) {
   double va[OPS_REG], vb[OPS_REG];
 #pragma unroll
@@ -189,8 +203,10 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
         v = va[k] - vb[k];
       else if (code == 2)
         v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - (SLIM ? t.k1[c] : t.k[c].x);
+      else if constexpr (SLIM)
+        v = __builtin_nan("");
       else
-        v = SLIM ? __builtin_nan("") : eval_op<FULL>(t, c, xrow);
+        v = eval_op<FULL>(t, c, xrow);
       if (v <= t.tol) v = 0.0;
       const double g = v * (v > 0.0 ? 1.0 : 0.0);
       const int col = MV_IDX(t.col[c], t.C, CK_CONS_COL);
@@ -199,7 +215,8 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
       acc3 += g;
     }
   }
-  for (int c = lane + 64 * OPS_REG; !SLIM && c < t.n_lane; c += 64) {
+  if constexpr (!SLIM)
+  for (int c = lane + 64 * OPS_REG; c < t.n_lane; c += 64) {
     double v = eval_op<FULL>(t, c, xrow);
     if (v <= t.tol) v = 0.0;
     const double g = v * (v > 0.0 ? 1.0 : 0.0);
