@@ -40,7 +40,10 @@ constexpr int CONS_T = MV_CONS_T;
 constexpr int CONS_W = CONS_T / 64;
 constexpr int VARY_ROWS_MAX = 32; // rows of one state per k_gen / k_cons workgroup (swept: 16/32/64)
 constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
-constexpr int SURV_T = 512;      // threads per survival workgroup (8 waves)
+#ifndef MV_SURV_T
+#define MV_SURV_T 512
+#endif
+constexpr int SURV_T = MV_SURV_T;  // threads per survival workgroup (8 waves)
 constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P + O = 963)
 constexpr int SURV_NLDS = 512;   // up to this N the dominance bitsets live in LDS, else in HBM
 constexpr int SURV_RMAX = 640;   // reference points
