@@ -7,7 +7,10 @@ one-hot consistency (utils.py:43-54), ``ml_scaler`` + classifier (fp32 MFMA), an
 min-max distance, for ALL initial states in one launch chain (``success_rate_3d`` and
 ``get_successful_attacks`` batch the states instead of looping per state).  The thresholding
 and the per-state / per-column means (``_objective_respected``, :86-119) are the same numpy
-as the reference.  There is no CPU fallback: without the engine library this raises.
+as the reference.  A constraints object without a device program, or a classifier that is
+not a Dense MLP, is evaluated by the user's own plugin (``evaluate`` / ``predict_proba``,
+objective_calculator.py:50,64) and the rest is scored on the device (``mv_objcalc_score``);
+nothing falls back to the oracle, and without the engine library this raises.
 """
 from __future__ import annotations
 
