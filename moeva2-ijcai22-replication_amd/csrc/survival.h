@@ -75,6 +75,33 @@ __host__ __device__ __forceinline__ int pow2_at_least(int n) {
   return p;
 }
 
+// Ascending bitonic sort of n (a power of two) 64-bit keys in LDS by the whole workgroup;
+// ends on a barrier.
+template <int T>
+__device__ __forceinline__ void bitonic_sort_u64(unsigned long long* k, int n) {
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (n >> 1); t += T) {
+        const int i = 2 * t - (t & (stride - 1));  // pair (i, i + stride), bit stride of i clear
+        const int j = i + stride;
+        const unsigned long long x = k[i], y = k[j];
+        if ((x > y) == ((i & size) == 0)) {
+          k[i] = y;
+          k[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// Niching ranks the last front's members inside their niches by counting over each niche's
+// members: quadratic in a niche's size.  When one niche holds more than this many members
+// (the first generations, whose population is copies of one initial state, put the whole
+// last front into one niche: 101 k cycles per state at configs[3], N = 963), one bitonic
+// sort of all the keys replaces the counting (~7 k cycles at 1024 keys).  Only the N >
+// SURV_NLDS instance, whose sort-key array is a power of two long.
+constexpr int NICHE_SORT_MIN = 256;
+
 // Byte offsets of the survival workspace inside the dynamic LDS block.
 struct SurvOff {
   unsigned F, ref, U, Uf, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
@@ -117,7 +144,9 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(sel, N * 4)
   TAKE(fstart, (N + 2) * 4)
   TAKE(iscal, (16 + SURV_TMAX / 64) * 4)
-  TAKE(sortk, (size_t)(N > Pperm ? N : Pperm) * 8)
+  // the sort keys; above SURV_NLDS a power of two for niching's bitonic sort (NICHE_SORT_MIN)
+  const int nsk = N > SURV_NLDS ? pow2_at_least(N) : N;
+  TAKE(sortk, (size_t)(nsk > Pperm ? nsk : Pperm) * 8)
   TAKE(perm, (size_t)Pperm * 4)
   const unsigned end = off;
   // the niching temporaries: inside the dominance bitsets when they fit, else appended
@@ -977,6 +1006,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       bestkr[n] = INT_MAX;
       fill[n] = 0;
     }
+    if (tid == 0) L.iscal[14] = 0;  // largest niche (the dominance counter is done)
     for (int l = tid; l < nlev; l += T) L.lround[l] = 0;
     // The counters above must be zero before ANY thread counts into them.  (Round 3 had no
     // barrier here: a thread of one wave could add its member to mcnt[n] / cnt[n] before the
@@ -990,7 +1020,8 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     // member order inside each niche: ascending (niche, member key, position); grank = rank
     for (int p = tid; p < Lc; p += T) {
       const unsigned key = rng.draw((uint32_t)p, (uint32_t)gen, TAG_NICHE_MEMBER).x;
-      atomicAdd(&mcnt[nich[p]], 1);
+      const int m_n = atomicAdd(&mcnt[nich[p]], 1) + 1;
+      if (NWMAX * 64 > SURV_NLDS && m_n > NICHE_SORT_MIN) atomicMax(&L.iscal[14], m_n);
       // (niche, member key, position); positions take 10 bits (N <= 1024)
       sk[p] = ((unsigned long long)nich[p] << 42) | ((unsigned long long)key << 10) | (unsigned)p;
     }
@@ -1004,14 +1035,31 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     for (int n = tid; n < RN; n += T) start[n] = mcnt[n];
     __syncthreads();
     block_scan_excl<T>(start, RN, wsum);
-    for (int p = tid; p < Lc; p += T) {
-      const int np_ = nich[p];
-      mem[start[np_] + atomicAdd(&fill[np_], 1)] = p;
+    const bool by_sort = NWMAX * 64 > SURV_NLDS && L.iscal[14] > NICHE_SORT_MIN;  // uniform
+    if (!by_sort) {
+      for (int p = tid; p < Lc; p += T) {
+        const int np_ = nich[p];
+        mem[start[np_] + atomicAdd(&fill[np_], 1)] = p;
+      }
     }
     __syncthreads();
     PHASE(17)
     // grank = rank of sk[p] among all keys = members of smaller niches (start) + rank inside
-    // its own niche, counted over that niche's members only
+    // its own niche.  The keys are distinct and niche-major, so that is sk[p]'s position in
+    // the sorted keys (by_sort), or counted over its niche's members only
+    if (by_sort) {
+      const int P2 = pow2_at_least(Lc);
+      for (int q = Lc + tid; q < P2; q += T) sk[q] = ~0ull;  // padding sorts last
+      __syncthreads();
+      bitonic_sort_u64<T>(sk, P2);
+      for (int r = tid; r < Lc; r += T) {
+        const int p = (int)(sk[r] & 1023ull);
+        const int np_ = nich[p];
+        grank[p] = r;
+        if (cnt[np_] == 0 && (unsigned long long)__double_as_longlong(dst[p]) == L.dmin[np_])
+          atomicMin(&bestkr[np_], r - start[np_]);
+      }
+    } else
     for (int p = tid; p < Lc; p += T) {
       const int np_ = nich[p];
       const unsigned long long kp = sk[p];

@@ -384,6 +384,43 @@ def test_survival_bit_exact_vs_oracle(N, n_survive):
             np.testing.assert_array_equal(state["extreme"][b].reshape(3, 3), ost[b].extreme)
 
 
+@pytest.mark.parametrize("N,n_survive,crowd", [(963, 643, 0), (963, 643, 1), (700, 400, 1),
+                                               (963, 643, 2)])
+def test_survival_bit_exact_one_long_front(N, n_survive, crowd):
+    """Every merged individual non-dominated (points on the plane f0 + f1 + f2 = 1, with
+    exact duplicates), so the last front is the whole population.  crowd 1: the points
+    bunched near one corner, so one niche holds ~300 members (N = 963: more than
+    NICHE_SORT_MIN = 256, so niching ranks the members by one bitonic sort of the keys;
+    N = 700: ~230, counted); crowd 2: every row identical (the first generations' copies of
+    one initial state), one niche holds all 963."""
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+
+    rng = np.random.default_rng(N + crowd)
+    B = 4
+    ref = energy_ref_dirs(3, 640, seed=1)
+    asp = np.full((1, 3), 1.0 / 3.0)
+    state = dict(ideal=np.full((B, 3), np.inf), worst=np.full((B, 3), -np.inf),
+                 extreme=np.zeros((B, 9)), has=np.zeros(B, np.int32))
+    ost = [mo.SurvivalState() for _ in range(B)]
+    for gen in range(2):
+        w = rng.dirichlet([0.3, 0.3, 8.0] if crowd else [1.0, 1.0, 1.0], size=(B, N))
+        F = np.round(w, 3)  # ties and duplicates
+        F[..., 2] = 1.0 - F[..., 0] - F[..., 1]
+        F[:, N // 2:N // 2 + 20] = F[:, :20]
+        if crowd == 2:
+            F[:] = F[:, :1]
+        got = _run_survive(F, ref, n_survive, 7, gen, state)
+        for b in range(B):
+            r = mo.survive(F[b], n_survive, ost[b], ref, asp, 0.05, 7, gen)
+            nr = len(np.concatenate(r.fronts))
+            assert got["nr"][b] == nr
+            assert len(r.fronts[-1]) > 512 or N < 900
+            np.testing.assert_array_equal(got["order"][b, :nr], np.concatenate(r.fronts))
+            np.testing.assert_array_equal(got["niche"][b, :nr], r.niche)
+            np.testing.assert_array_equal(got["dist"][b, :nr], r.dist)
+            np.testing.assert_array_equal(got["surv"][b], r.survivors)
+
+
 def test_survival_bit_exact_on_clone_heavy_botnet_states(golden):
     """Survival inputs of real botnet attack generations where the merged population is
     mostly clones (41-93 distinct objective rows of 303, one front of ~275 individuals, so
