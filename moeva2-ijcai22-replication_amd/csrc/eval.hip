@@ -947,6 +947,11 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
   float* H = A0;  // hidden ping-pong, aliases the layer-0 chunks
   for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
   if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  // the hidden layers' biases in LDS too (their epilogues read one per output element: from
+  // global memory each layer's epilogue waited out an L2 round trip)
+  float* hbl = bl + nout;
+  for (int l = 1, off = 0; l + 1 < nl; off += p.dims[l + 1], ++l)
+    for (int q = tid; q < p.dims[l + 1]; q += 256) hbl[off + q] = p.bias[l][q];
   double* sS = (double*)(smem + mlp2_sc_off(p));
   double* sM = sS + K0;
   if (DIRECT)
@@ -1237,7 +1242,7 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
 #undef M2_CHUNK_STORE
     if (ph) phq[3] = clock64();
     // hidden layers: layer l writes H[l & 1]
-    for (int l = 0; l + 1 < nl; ++l) {
+    for (int l = 0, hoff = 0; l + 1 < nl; hoff += l > 0 ? p.dims[l + 1] : 0, ++l) {
       const int N = p.dims[l + 1];
       const TileMap m = tile_map(N >> 4, wave);
       if (l > 0) {
@@ -1273,7 +1278,7 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
                   bv = b1[cj][rt][j];
                 }
               } else {
-                bv = p.bias[l][col];
+                bv = hbl[hoff + col];
               }
               const float v = acc[cj][rt][j] + bv;
               out[row * hld + col] = v > 0.f ? v : 0.f;

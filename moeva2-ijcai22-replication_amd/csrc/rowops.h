@@ -575,9 +575,16 @@ __host__ __device__ inline int mlp2_hmax(const DProblem& p) {
   for (int l = 1; l < p.n_layers; ++l) h = p.dims[l] > h ? p.dims[l] : h;
   return h;
 }
+// head: row states (256 B), the final layer's weights and bias, the hidden layers' biases
+__host__ __device__ inline int mlp2_hidden_bias_floats(const DProblem& p) {
+  int n = 0;
+  for (int l = 1; l + 1 < p.n_layers; ++l) n += p.dims[l + 1];
+  return n;
+}
 __host__ __device__ inline size_t mlp2_head(const DProblem& p) {
   const int nl = p.n_layers;
-  return 256 + (((size_t)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~(size_t)15);
+  return 256 + (((size_t)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl] + mlp2_hidden_bias_floats(p)) *
+                     4 + 15) & ~(size_t)15);
 }
 // The hidden ping-pong H aliases the layer-0 chunk buffers (free once layer 0 is done), so
 // four workgroups fit a CU's LDS.
