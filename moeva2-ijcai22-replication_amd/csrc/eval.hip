@@ -86,9 +86,16 @@ hipError_t release_rows(int slot, hipStream_t stream) {
   return hipEventRecord(g_rings[dev].ev[slot], stream);
 }
 
-// The draws of one offspring row (one row per lane): packed parents (own | oth << 16), the
-// two crossover subsets' draws, and the mutations -- count | overflow << 3 | (last position
-// + 1) << 4, positions and mutated values (crossed parent value through mutate_gene).
+// The draws of one offspring row: packed parents (own | oth << 16) and the two crossover
+// subsets' draws on the row's lane k; its mutations on lanes 4 k + q (a wave holds <= 16
+// rows): lane 4 k + q takes the q-th draw of row k's geometric-gap process (Philox index
+// row * MUT_J + q, TAG_MUT_MASK), the gaps' prefix sum over the row's four lanes gives the
+// positions -- the same draws and positions as walking them one after another, computed in
+// one parallel round -- and the lane mutates its position's crossed parent value
+// (mutate_gene).  mut_v (row lane k): count | overflow << 3; a row with more than CAP
+// mutations (its 5th draw is still inside the genes, checked on lane 4 k + 3) is redone by
+// the caller with every mutation.  mposv / mvalv (lane 4 k + q): the stored gene (-1: a
+// fixed gene of the compact layout, whose mutation is the identity) and its new value.
 // (A separate one-row-per-lane kernel computing these ahead of k_gen was measured slower:
 // its serial Philox / pow chains sit on the generation's critical path.)
 // `preload` runs once the mating is known, before the mutation draws: the caller issues the
@@ -98,9 +105,8 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
                                           const int irow, const bool mine, const int gen,
                                           const bool sbx, const uint32_t* geo, const int* ginfo,
                                           const int* cmap, const double* gin, const Rng& rng,
-                                          int& par_v,
-                                          int& cx0_v, int& cx1_v, int& mut_v, int (&mpos)[CAP],
-                                          double (&mval)[CAP], const int2 pre_pr,
+                                          int& par_v, int& cx0_v, int& cx1_v, int& mut_v,
+                                          int& mposv, double& mvalv, const int2 pre_pr,
                                           Preload&& preload) {
   const int V = p.V, Vr = p.Vr;  // stored genes, genes the draws are defined over
   if (mine) {
@@ -117,78 +123,57 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
     }
   }
   preload();
-  // (1) mutation positions (of the Vr genes) and their PM uniforms
-  const float lq = __log2f(1.0f - 1.0f / (float)Vr);
-  bool going = mine && !sbx;
-  int pos = -1, cnt = 0, ovf = 0;
-  double mu[CAP] = {};
-#pragma unroll 1
-  for (int j = 0; j <= CAP && __ballot(going); ++j) {
-    bool have = false;
-    double u = 0.0;
-    if (going) {
-      const u32x4 w = rng.draw((uint32_t)(irow * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-      pos += 1 + geo_gap(geo, Vr, w.x, lq);
-      if (pos >= Vr) {
-        going = false;
-      } else if (j == CAP) {
-        ovf = 1;
-        going = false;
-      } else {
-        have = true;
-        u = u53(w.y, w.z);
-        cnt = j + 1;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < CAP; ++q)
-      if (have && q == j) {
-        mpos[q] = pos;
-        mu[q] = u;
-      }
-  }
-  // (2) + (3) one (row, mutation) pair per lane: lane 4 k + q loads row k's crossed parent
-  // value and gene bounds at its q-th mutated position and mutates it -- one pow pair deep
-  // instead of a loop over the wave's largest mutation count (a wave holds <= 16 rows).
-  // The position is mapped to its stored gene (cmap); a fixed gene of the compact layout
-  // (-1) is not stored and its mutation is the identity (integer gene, xl == xu == value),
-  // so the row keeps the draw and drops the write.
   static_assert(CAP == 4, "row_draws maps 16 rows x 4 mutations onto the 64 lanes");
-  const double* gl = a.s.gl + (size_t)b * V;
-  const double* gu = a.s.gu + (size_t)b * V;
   const int lane = threadIdx.x & 63;
   const int kk = lane >> 2, qq = lane & 3;
-  int pq = -1;
+  // (1) draw qq of row kk: its gap and PM uniform, then the positions (prefix sums of the
+  // 1 + gap steps from -1 within the row's four lanes)
+  const int irow_k = __shfl(irow, kk);
+  const bool live = __shfl(mine ? 1 : 0, kk) != 0 && !sbx;
+  const float lq = __log2f(1.0f - 1.0f / (float)Vr);
+  int st = 0;
   double uq = 0.0;
-#pragma unroll
-  for (int q = 0; q < CAP; ++q) {
-    const int pv = __shfl(mpos[q], kk);
-    const double uv = __shfl(mu[q], kk);
-    if (q == qq) {
-      pq = pv;
-      uq = uv;
-    }
+  if (live) {
+    const u32x4 w = rng.draw((uint32_t)(irow_k * MUT_J + qq), (uint32_t)gen, TAG_MUT_MASK);
+    st = 1 + geo_gap(geo, Vr, w.x, lq);
+    uq = u53(w.y, w.z);
   }
-  const int cntk = __shfl(cnt, kk), park = __shfl(par_v, kk);
+  {
+    const int t1 = __shfl(st, (lane + 63) & 63);
+    st += qq >= 1 ? t1 : 0;
+    const int t2 = __shfl(st, (lane + 62) & 63);
+    st += qq >= 2 ? t2 : 0;
+  }
+  const int pq = st - 1;                // position of draw qq (increasing in qq)
+  const bool hit = live && pq < Vr;     // the hits of a row are its lanes 0 .. count - 1
+  int ovf = 0;
+  if (qq == CAP - 1 && hit) {           // four mutations: does a fifth fall inside?
+    const u32x4 w = rng.draw((uint32_t)(irow_k * MUT_J + CAP), (uint32_t)gen, TAG_MUT_MASK);
+    ovf = pq + 1 + geo_gap(geo, Vr, w.x, lq) < Vr ? 1 : 0;
+  }
+  const unsigned long long hm = __ballot(hit), om = __ballot(ovf != 0);
+  // (2) + (3) lane 4 k + q loads row k's crossed parent value and gene bounds at its
+  // position and mutates it -- one pow pair deep for the whole wave.  The position is mapped
+  // to its stored gene (cmap); a fixed gene of the compact layout (-1) is not stored and its
+  // mutation is the identity (integer gene, xl == xu == value): the draw stays, the write
+  // goes.
+  const double* gl = a.s.gl + (size_t)b * V;
+  const double* gu = a.s.gu + (size_t)b * V;
+  const int park = __shfl(par_v, kk);
   const int c0k = __shfl(cx0_v, kk), c1k = __shfl(cx1_v, kk);
-  const int cq = cmap[MV_IDX(pq < 0 ? 0 : pq, Vr, CK_GEN_MUTPOS)];  // unconditional loads
+  const int pc = hit ? pq : 0;
+  const int cq = cmap[MV_IDX(pc, Vr, CK_GEN_MUTPOS)];  // unconditional loads
   const int mp = MV_IDX(cq < 0 ? 0 : cq, V, CK_GEN_MUTPOS);
   const int gi = ginfo[mp];
   const int mrow = MV_IDX(swapped_packed(gi, c0k, c1k) ? (park >> 16) : (park & 0xFFFF),
                           a.in_rows, CK_GEN_MUTROW);
   double xv = gin[MV_IDX((size_t)mrow * V + mp, (long long)a.in_rows * V, CK_AT_MUTLOAD)];
   const double lo = gl[MV_IDX(mp, V, CK_AT_BOUNDS)], hi = gu[MV_IDX(mp, V, CK_AT_BOUNDS)];
-  if (qq < cntk) xv = mutate_gene(xv, lo, hi, (gi & 3) == 0, uq, a.eta);
-  int last = -1;
-#pragma unroll
-  for (int q = 0; q < CAP; ++q)
-    if (q < cnt) last = mpos[q];
-#pragma unroll
-  for (int q = 0; q < CAP; ++q) {  // back to the row lanes: values and stored positions
-    mval[q] = __shfl(xv, (lane * 4 + q) & 63);
-    mpos[q] = __shfl(cq, (lane * 4 + q) & 63);
-  }
-  mut_v = cnt | (ovf << 3) | ((last + 1) << 4);
+  if (hit) xv = mutate_gene(xv, lo, hi, (gi & 3) == 0, uq, a.eta);
+  mposv = hit ? cq : -1;
+  mvalv = xv;
+  const int cnt = __popcll((hm >> (4 * (lane & 15))) & 0xFull);  // row lanes k < 16
+  mut_v = cnt | ((int)((om >> (4 * (lane & 15) + 3)) & 1ull) << 3);
 }
 
 // k_gen: variation (mode 1) or gene load (mode 0), the child genes to the pool, the fp32
@@ -284,13 +269,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   // this wave's rows: lane k holds row k's packed parents (own | oth << 16), crossover
   // draws, destination and mutations (count | overflow << 3 | (last position + 1) << 4)
   int par_v = 0, cx0_v = 0, cx1_v = 0, mut_v = 0;
-  int mpos[MUT_CAP];
-  double mval[MUT_CAP];
-#pragma unroll
-  for (int q = 0; q < MUT_CAP; ++q) {
-    mpos[q] = -1;
-    mval[q] = 0.0;
-  }
+  int mposv = -1;        // lane 4 k + q: row k's q-th mutation (stored gene, -1 none / fixed)
+  double mvalv = 0.0;    //               and its value
   const double* gin = a.genes_in + (size_t)b * a.in_rows * V;
   const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
   const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
@@ -312,7 +292,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   };
   if (a.mode == 1) {
     row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, s_cmap, gin, rng, par_v,
-                       cx0_v, cx1_v, mut_v, mpos, mval, pre_pr, preload);
+                       cx0_v, cx1_v, mut_v, mposv, mvalv, pre_pr, preload);
   } else {
     if (mine) par_v = irow | (irow << 16);
     preload();
@@ -405,7 +385,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
                   a.sbx_eta, lane, (int*)(sb + 64 * NT * 8), (double*)sb);
       mutate_row_full<NT>(x, s_geo, s_ginfo, s_cmap, sgl, sgu, p.Vr, i, rng, gen, a.eta, lane);
     } else if (a.mode == 1) {  // apply the row's cached mutations
-      apply_row_mutations<NT>(x, rdl(mut_v, k) & 7, mpos, mval, k, lane);
+      apply_row_mutations<NT, MUT_CAP>(x, rdl(mut_v, k) & 7, mposv, mvalv, k, lane);
     }
     finish_row(k, x);
   }

@@ -720,18 +720,18 @@ __device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, 
   }
 }
 
-// The cached mutations of row k (positions / values held by lane k): each position is
-// wave-uniform, so its register index t = pos / 64 is a scalar branch and only that
-// register is updated, on lane pos % 64.
+// The cached mutations of row k (position / value q held by lane 4 k + q, row_draws): each
+// position is wave-uniform, so its register index t = pos / 64 is a scalar branch and only
+// that register is updated, on lane pos % 64.
 template <int NT, int CAP>
-__device__ __forceinline__ void apply_row_mutations(double* x, int nmut, const int (&mpos)[CAP],
-                                                    const double (&mval)[CAP], int k, int lane) {
+__device__ __forceinline__ void apply_row_mutations(double* x, int nmut, int mposv, double mvalv,
+                                                    int k, int lane) {
 #pragma unroll
   for (int q = 0; q < CAP; ++q) {
-    const int pr = rdl(mpos[q], k);  // stored gene; -1: a fixed gene (compact layout), no-op
+    const int pr = rdl(mposv, 4 * k + q);  // stored gene; -1: a fixed gene (compact layout)
     if (q < nmut && pr >= 0) {
       const int pos = MV_IDX(pr, 64 * NT, CK_GEN_APPLY);
-      const double y = rdl_d(mval[q], k);
+      const double y = rdl_d(mvalv, 4 * k + q);
       const int tt = pos >> 6;
       const bool me = lane == (pos & 63);
 #pragma unroll
