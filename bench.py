@@ -240,46 +240,15 @@ def load_traffic(workload):
     return {}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="rq1.botnet.static", choices=sorted(WORKLOADS))
-    ap.add_argument("--n-gen", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--groups", type=int, default=None,
-                    help="state groups (streams) of the timed attack; default: engine's choice. "
-                         "--groups 1 makes every launch cover all states, like the roofline "
-                         "pass, so rocprofv3 averages compare 1:1 with the bench's event times")
-    ap.add_argument("--mode", default="auto", choices=["auto", "chain"],
-                    help="attack schedule (the per-phase kernel chain; the whole-attack "
-                         "kernel was retired)")
-    ap.add_argument("--crossover", default="two_point", choices=["two_point", "sbx"])
-    ap.add_argument("--mlp-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="classifier precision: fp32 (parity, default) or the bf16 perf mode "
-                         "(a separately labelled line: f1 is not Keras's value)")
-    ap.add_argument("--shard", action="store_true",
-                    help="strong scaling: split the states over the ranks")
-    ap.add_argument("--cpu-gens", type=int, default=300)
-    args = ap.parse_args()
-
-    if args.groups:
-        os.environ["MV_GROUPS"] = str(args.groups)
+def run_workload(name, w, args, device, world, rank, steps, warmup, bf16, crossover,
+                 profile_gens=None, warm_gens=None):
+    """Bind the workload's states, time `steps` whole attacks (after `warmup` untimed ones of
+    warm_gens generations, default the full budget), then the per-kernel HIP-event pass (one
+    state group, profile_gens generations, default the full budget).  Returns the result
+    dict (rank 0; None on the other ranks)."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = local if world > 1 else 0
-    torch.cuda.set_device(device)
-    w = dict(WORKLOADS[args.workload])
-    if args.n_gen:
-        w["n_gen"] = args.n_gen
     from moeva2_amd.attacks.moeva2.moeva2 import history_mode
     from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
     from moeva2_amd.distributed import generate_sharded, shard_bounds
@@ -287,9 +256,8 @@ def main():
     t_load = time.perf_counter()
     eng, c = build_engine(w, device)
     eng.set_attack_mode(args.mode)
-    eng.set_crossover(args.crossover)
-    eng.set_mlp_precision(args.mlp_dtype)
-    bf16 = args.mlp_dtype == "bf16"
+    eng.set_crossover(crossover)
+    eng.set_mlp_precision("bf16" if bf16 else "fp32")
     X_all = load_states(w)
     # weak scaling (default): the workload's state set tiled x N (rank r owns copy r);
     # strong (--shard): the workload's states split over the ranks.  Either way the step is
@@ -315,10 +283,11 @@ def main():
     torch.cuda.synchronize()
     load_s = time.perf_counter() - t_load
     seed = 42  # the configs' seed, every state (moeva2.py:163)
+    n_gen_run = [G]
 
     def attack(xs, mcs):  # the rank's shard is bound once, outside the timed region
         assert xs.shape[0] == B
-        eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
+        eng.attack_run(n_gen_run[0], P, O, seed, ref, 0.05, hmode)
         eng.attack_population(genes, F)
         return genes, F
 
@@ -328,15 +297,19 @@ def main():
     def step():
         return generate_sharded(attack, X_glob, 1, empty=empty)
 
-    for i in range(args.warmup):
+    # warm-up attacks allocate the attack's buffers (their sizes do not depend on the budget
+    # without history, so a short warm-up suffices then)
+    n_gen_run[0] = warm_gens if (warm_gens and not hmode) else G
+    for i in range(warmup):
         step()
         torch.cuda.synchronize()
-        log(f"[rank {rank}] warmup {i + 1}/{args.warmup} done")
+        log(f"[rank {rank}] {name}: warmup {i + 1}/{warmup} done")
+    n_gen_run[0] = G
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         out = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -347,22 +320,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert out[0].shape == (states_total, P, V)
-    log(f"[rank {rank}] timed {args.steps} steps in {elapsed:.3f}s")
+    log(f"[rank {rank}] {name}: timed {steps} steps in {elapsed:.3f}s")
 
     evals_per_state = P + (G - 1) * O
-    total_evals = states_total * evals_per_state * args.steps
+    total_evals = states_total * evals_per_state * steps
     value = total_evals / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
+    ms_per_step = 1000.0 * elapsed / steps
 
     # ---- roofline of the dominant kernel, measured live with HIP events that the engine
     # records on the bench stream around every launch (one state group, so each launch
     # covers all states of the rank like the rocprofv3 pass of the same command)
     if rank != 0:  # only rank 0 reports (it always owns states); the others are done
-        if world > 1:
-            dist.destroy_process_group()
-        return
+        return None
     eng.set_profiling(True)
-    eng.attack_run(G, P, O, seed, ref, 0.05, hmode)
+    eng.attack_run(profile_gens or G, P, O, seed, ref, 0.05, hmode)
     torch.cuda.synchronize()
     kt = eng.kernel_times()
     eng.set_profiling(False)
@@ -396,69 +367,68 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of THIS workload and
     # schedule (tools/pmc_traffic.py: (2*FETCH_SIZE + WRITE_SIZE) KiB, gfx950 correction)
     traffic = {}
-    if args.crossover == "two_point" and not bf16:
-        traffic = load_traffic(args.workload)
+    if crossover == "two_point" and not bf16:
+        traffic = load_traffic(name)
 
-    def hbm(name, bytes_launch, ms, key):
+    def hbm(kname, bytes_launch, ms, key):
         gbs = bytes_launch / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs / HBM_PEAK_GBS, "traffic": traffic.get(key), "kernel": name,
+                "frac": gbs / HBM_PEAK_GBS, "traffic": traffic.get(key), "kernel": kname,
                 "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": ms}
 
-    if True:
-        ng = max(kt["generations"], 1)
-        gen_ms = kt["gen_ms"] / ng
-        cons_ms = kt["cons_ms"] / ng
-        mlp_ms = kt["mlp_ms"] / ng
-        surv_ms = kt["survive_ms"] / ng
-        # achieved / frac on the FLOPs the kernel executes (immutable features folded into
-        # the per-state bias); the full-chain algorithmic rate is reported beside it
-        mlp_tfs = exec_flops * rows / (mlp_ms * 1e-3) / 1e12
-        mlp_tfs_alg = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
-        mlp_peak = MFMA_BF16_PEAK_TFS if bf16 else MFMA_F32_PEAK_TFS
-        kernels = {
-            "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows,
-                         gen_ms, "k_gen"),
-            "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
-                          "k_cons"),
-            "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": mlp_peak,
-                      "unit": "TFLOP/s", "frac": mlp_tfs / mlp_peak,
-                      "traffic": traffic.get("k_mlp"),
-                      "kernel": "%s (%s MFMA Dense chain)" % (kt["mlp_kernel"],
-                                                               "bf16" if bf16 else "fp32"),
-                      "achieved_algorithmic": mlp_tfs_alg,
-                      "algorithmic_flops_per_launch": eval_flops * rows,
-                      "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},
-            "k_survive": hbm("k_survive (R-NSGA-III survival + tournament; latency-bound)",
-                             surv_bytes_state * B, surv_ms, "k_survive"),
-        }
-        per_gen = {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
-        # LCLD-shaped rows run k_narrow (csrc/narrow.h narrow_ok): variation + decode + f2 +
-        # constraint program in ONE launch; IDENT wave-per-row problems (the botnet shape) run
-        # k_genc (k_gen and k_cons as two phases of one launch).  Either way the engine's
-        # "k_gen" events bracket the one launch and its "k_cons" events an empty step, so the
-        # pair is reported as one kernel with the combined algorithmic bytes.
-        rk = kt.get("row_kernel", "k_gen+k_cons")
-        if rk == "k_narrow":
-            hist_b = {"full": 8 * (3 + prog.C), "reduced": 24}.get(w["history"], 0)
-            nb = 2 * V * 8 + Dm4 * 4 + 16 + hist_b
-            kernels.pop("k_gen")
-            kernels.pop("k_cons")
-            kernels["k_narrow"] = hbm("k_narrow (crossover + mutation + ML row + distance + "
-                                      "constraint program, one lane per row)", nb * rows,
-                                      gen_ms + cons_ms, "k_narrow")
-            per_gen = {"k_narrow": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
-        elif rk == "k_genc":
-            # parents read + child written once (2*V*8) + f2 + f3; phase 2 re-reads the child
-            # rows its own workgroup just wrote (L2/MALL hits, not algorithmic HBM bytes)
-            nb = gen_bytes + 8
-            kernels.pop("k_gen")
-            kernels.pop("k_cons")
-            kernels["k_genc"] = hbm("k_genc (crossover + mutation + distance, then the "
-                                    "constraint program over the same rows; one launch)",
-                                    nb * rows, gen_ms + cons_ms, "k_genc")
-            per_gen = {"k_genc": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
-        per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+    ng = max(kt["generations"], 1)
+    gen_ms = kt["gen_ms"] / ng
+    cons_ms = kt["cons_ms"] / ng
+    mlp_ms = kt["mlp_ms"] / ng
+    surv_ms = kt["survive_ms"] / ng
+    # achieved / frac on the FLOPs the kernel executes (immutable features folded into
+    # the per-state bias); the full-chain algorithmic rate is reported beside it
+    mlp_tfs = exec_flops * rows / (mlp_ms * 1e-3) / 1e12
+    mlp_tfs_alg = eval_flops * rows / (mlp_ms * 1e-3) / 1e12
+    mlp_peak = MFMA_BF16_PEAK_TFS if bf16 else MFMA_F32_PEAK_TFS
+    kernels = {
+        "k_gen": hbm("k_gen (crossover + mutation + ML row + distance)", gen_bytes * rows,
+                     gen_ms, "k_gen"),
+        "k_cons": hbm("k_cons (constraint program, f3)", cons_bytes * rows, cons_ms,
+                      "k_cons"),
+        "k_mlp": {"bound": "mfma", "achieved": mlp_tfs, "peak": mlp_peak,
+                  "unit": "TFLOP/s", "frac": mlp_tfs / mlp_peak,
+                  "traffic": traffic.get("k_mlp"),
+                  "kernel": "%s (%s MFMA Dense chain)" % (kt["mlp_kernel"],
+                                                           "bf16" if bf16 else "fp32"),
+                  "achieved_algorithmic": mlp_tfs_alg,
+                  "algorithmic_flops_per_launch": eval_flops * rows,
+                  "executed_flops_per_launch": exec_flops * rows, "avg_launch_ms": mlp_ms},
+        "k_survive": hbm("k_survive (R-NSGA-III survival + tournament + variation plan; "
+                         "latency-bound)", surv_bytes_state * B, surv_ms, "k_survive"),
+    }
+    per_gen = {"k_gen": gen_ms, "k_cons": cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+    # LCLD-shaped rows run k_narrow (csrc/narrow.h narrow_ok): variation + decode + f2 +
+    # constraint program in ONE launch; IDENT wave-per-row problems (the botnet shape) run
+    # k_genc (k_gen and k_cons as two phases of one launch).  Either way the engine's
+    # "k_gen" events bracket the one launch and its "k_cons" events an empty step, so the
+    # pair is reported as one kernel with the combined algorithmic bytes.
+    rk = kt.get("row_kernel", "k_gen+k_cons")
+    if rk == "k_narrow":
+        hist_b = {"full": 8 * (3 + prog.C), "reduced": 24}.get(w["history"], 0)
+        nb = 2 * V * 8 + Dm4 * 4 + 16 + hist_b
+        kernels.pop("k_gen")
+        kernels.pop("k_cons")
+        kernels["k_narrow"] = hbm("k_narrow (crossover + mutation + ML row + distance + "
+                                  "constraint program, one lane per row)", nb * rows,
+                                  gen_ms + cons_ms, "k_narrow")
+        per_gen = {"k_narrow": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+    elif rk == "k_genc":
+        # parents read + child written once (2*V*8) + f2 + f3; phase 2 re-reads the child
+        # rows its own workgroup just wrote (L2/MALL hits, not algorithmic HBM bytes)
+        nb = gen_bytes + 8
+        kernels.pop("k_gen")
+        kernels.pop("k_cons")
+        kernels["k_genc"] = hbm("k_genc (crossover + mutation + distance, then the "
+                                "constraint program over the same rows; one launch)",
+                                nb * rows, gen_ms + cons_ms, "k_genc")
+        per_gen = {"k_genc": gen_ms + cons_ms, "k_mlp": mlp_ms, "k_survive": surv_ms}
+    per_gen["dominant"] = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
     dom = per_gen["dominant"]
     if args.shard:
         par = (f"generate_sharded: {B_all} states split over {world} rank(s) ({B} on rank "
@@ -466,41 +436,127 @@ def main():
     else:
         par = (f"generate_sharded: the {B_all} states tiled x{world} = {states_total}, "
                f"{B} per rank; one all_gather of the final populations")
-
     result = {
         "metric": "candidate fitness evals/sec (whole node) + attack wall-clock per 1k states",
         "value": value,
         "unit": "evals/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": steps,
+        "warmup": warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "strong" if args.shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": data_note(w, B_all),
-        "config": {"workload": args.workload, "states": states_total, "states_per_gpu": B,
+        "config": {"workload": name, "states": states_total, "states_per_gpu": B,
                    "pop_size": P, "n_offsprings": O, "n_gen": G, "norm": w["norm"],
                    "history": w["history"], "evals_per_state": evals_per_state,
                    "classifier_dtype": ("bf16 perf mode (bf16 MFMA, fp32 accumulate; not a "
                                         "parity result)" if bf16 else "f32 (MFMA)"),
-                   "crossover": args.crossover,
+                   "crossover": crossover,
                    "genes_stored": int(V) - n_fixed,
                    "schedule": "per-phase kernel chain",
                    "parallelism": par},
-        "attack_wall_clock_per_1k_states_s": elapsed / args.steps / states_total * 1000.0,
+        "attack_wall_clock_per_1k_states_s": elapsed / steps / states_total * 1000.0,
         "load_s": load_s,
         "roofline": kernels[dom],
         "kernels": kernels,
         "kernels_avg_ms_per_generation": per_gen,
+        "kernel_times_generations": ng,
         "algorithmic_per_eval": {"bytes": eval_bytes, "flops": eval_flops,
                                  "executed_flops": exec_flops},
     }
-    if rank == 0 and not args.no_cpu_baseline and world == 1 and \
-            not w["model"].startswith("synthetic:"):
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_gens)
+    del eng
+    return result
+
+
+# The other BASELINE.json configs, one full-config attack each after the headline (N = 1):
+# (key, workload, classifier dtype, warm-up generations, profiled generations)
+EXTRA_CONFIGS = [
+    ("configs[0]", "rq1.lcld.static", "fp32", None, None),
+    ("configs[2]", "rq4.lcld.moeva_augmented", "fp32", None, None),
+    ("configs[3]", "synthetic.lcld.scaleout", "fp32", 3, 6),
+    ("configs[4]", "synthetic.botnet.wide", "fp32", 3, 10),
+    ("configs[4] bf16", "synthetic.botnet.wide", "bf16", 3, 10),
+]
+
+
+def extra_line(key, r):
+    """The compact summary of one extra config's result."""
+    dom = r["kernels_avg_ms_per_generation"]["dominant"]
+    return {"value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+            "steps": r["steps"], "workload": r["config"]["workload"],
+            "states": r["config"]["states"], "pop_size": r["config"]["pop_size"],
+            "n_offsprings": r["config"]["n_offsprings"], "n_gen": r["config"]["n_gen"],
+            "history": r["config"]["history"],
+            "classifier_dtype": r["config"]["classifier_dtype"],
+            "dominant_kernel": dom, "roofline": r["roofline"],
+            "kernels_avg_ms_per_generation": r["kernels_avg_ms_per_generation"],
+            "kernel_times_generations": r["kernel_times_generations"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="rq1.botnet.static", choices=sorted(WORKLOADS))
+    ap.add_argument("--n-gen", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs' lines (N = 1 default: one full-config "
+                         "attack each of configs[0], [2], [3], [4] after the headline)")
+    ap.add_argument("--groups", type=int, default=None,
+                    help="state groups (streams) of the timed attack; default: engine's choice. "
+                         "--groups 1 makes every launch cover all states, like the roofline "
+                         "pass, so rocprofv3 averages compare 1:1 with the bench's event times")
+    ap.add_argument("--mode", default="auto", choices=["auto", "chain"],
+                    help="attack schedule (the per-phase kernel chain; the whole-attack "
+                         "kernel was retired)")
+    ap.add_argument("--crossover", default="two_point", choices=["two_point", "sbx"])
+    ap.add_argument("--mlp-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="classifier precision: fp32 (parity, default) or the bf16 perf mode "
+                         "(a separately labelled line: f1 is not Keras's value)")
+    ap.add_argument("--shard", action="store_true",
+                    help="strong scaling: split the states over the ranks")
+    ap.add_argument("--cpu-gens", type=int, default=300)
+    args = ap.parse_args()
+
+    if args.groups:
+        os.environ["MV_GROUPS"] = str(args.groups)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = local if world > 1 else 0
+    torch.cuda.set_device(device)
+    w = dict(WORKLOADS[args.workload])
+    if args.n_gen:
+        w["n_gen"] = args.n_gen
+    bf16 = args.mlp_dtype == "bf16"
+    result = run_workload(args.workload, w, args, device, world, rank, args.steps, args.warmup,
+                          bf16, args.crossover)
     if rank == 0:
+        if not args.no_cpu_baseline and world == 1 and not w["model"].startswith("synthetic:"):
+            result["cpu_baseline"] = cpu_baseline(w, args.cpu_gens)
+        # the other BASELINE configs (single GPU, default N = 1 run only): one timed
+        # full-config attack each, with its own dominant kernel and roofline
+        if world == 1 and not args.no_configs and not args.n_gen and args.workload == \
+                "rq1.botnet.static" and args.crossover == "two_point" and not bf16:
+            extra = {}
+            for key, name, dt, wg, pg in EXTRA_CONFIGS:
+                torch.cuda.empty_cache()
+                r = run_workload(name, dict(WORKLOADS[name]), args, device, 1, 0, 1, 1,
+                                 dt == "bf16", "two_point", profile_gens=pg, warm_gens=wg)
+                extra[key] = extra_line(key, r)
+                log(f"{key} {name} {dt}: {r['value'] / 1e6:.1f} M evals/s")
+            result["configs"] = extra
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -110,6 +110,8 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
  * genes dev [B][n][V] -> x dev [B][n][D] with the bound states' x_init. */
 int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* stream);
 
+/* Entry points taking device buffers fail with MV_ERR_ARG when a buffer is device memory of
+ * another GPU than the engine's (or objcalc's). */
 /* Constraints.evaluate (numpy path: values <= tol set to 0) on ML-space rows:
  * x dev [n][D] -> G dev [n][C].  Works on an engine created without a model. */
 int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream);
@@ -243,6 +245,18 @@ int mv_attack_history(mv_engine* e, double* hist, void* stream);
  * every gene.  stored (may be NULL) [V] receives 1 for a stored gene, 0 for a fixed one;
  * *n_stored the stored count (= V when nothing is fixed, or MV_COMPACT=0). */
 int mv_get_stored_genes(mv_engine* e, int32_t* stored, int32_t* n_stored);
+/* The layout mv_set_states would derive for B states (host arrays as mv_set_states; host
+ * computation only, no device work): stored [V] 1 / 0 and *n_stored, as mv_get_stored_genes
+ * reports after binding them. */
+int mv_gene_layout(mv_engine* e, int32_t B, const double* x_init, const double* xl,
+                   const double* xu, int32_t* stored, int32_t* n_stored);
+/* Fix the layout of the following mv_set_states calls: stored [V] (1 = stored) as
+ * mv_gene_layout returned it for the WHOLE job, so a job split into batches or shards
+ * (Moeva2.generate_sharded) runs every state in the same layout -- a state's f1 / f2
+ * summation order, hence its trajectory, then does not depend on which states share its
+ * batch.  mv_set_states fails with MV_ERR_ARG when an unstored gene is not fixed in a bound
+ * state.  stored = NULL returns to deriving the layout from each bound batch (default). */
+int mv_set_gene_layout(mv_engine* e, const int32_t* stored, int32_t V);
 /* Per-kernel timing of the last mv_attack_run when enabled (one state group then): HIP
  * events recorded on the run's stream around the row kernel(s), the classifier and
  * k_survive of every generation (summed ms). */

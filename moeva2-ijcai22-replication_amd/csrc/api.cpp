@@ -68,6 +68,19 @@ __global__ void k_fill_i(int* p, size_t n, int v) {
     p[i] = v;
 }
 
+// True unless `p` is known device memory of a GPU other than `dev` (host or unregistered
+// pointers pass: the kernels' own faults report those).  Entry points taking buffers of
+// another GPU would otherwise run on `dev` with peer pointers and no cross-device order.
+bool on_device(const void* p, int dev) {
+  if (!p) return true;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return true;
+  }
+  return at.type != hipMemoryTypeDevice || at.device == dev;
+}
+
 }  // namespace
 
 // fp32 -> bf16 bits, round to nearest even (NaN stays a quiet NaN)
@@ -105,6 +118,9 @@ struct mv_engine {
   // are what mv_attack_run reads.
   bool compact = false;
   std::vector<int> stored;           // the compact layout's stored genes
+  // mv_set_gene_layout: the layout the next mv_set_states uses (empty: derive it from the
+  // bound batch); a caller that splits one job into batches passes the whole job's layout
+  std::vector<int> layout_req;
   DProblem pc{};
   std::vector<void*> compact_allocs;  // pc's tables (kept while the stored set is unchanged)
   DStates sc{};
@@ -129,6 +145,11 @@ struct mv_engine {
   int* pop_slot = nullptr;
   int* free_slot = nullptr;
   int* parents = nullptr;
+  // k_genc attacks: the variation plan k_survive writes for the next generation (VPlan)
+  bool has_plan = false;
+  int4* plan_hdr = nullptr;
+  int* plan_mw = nullptr;
+  double* plan_mu = nullptr;
   double *ideal = nullptr, *worst = nullptr, *extreme = nullptr;
   int* has_ext = nullptr;
   double* ref = nullptr;
@@ -559,20 +580,29 @@ static RowsArgs base_rows(const mv_engine* e, bool attack = false);
 // every state (crossover swaps equal values, a mutation is clamped back to the bound).  Such
 // genes exist only in IDENT problems here (botnet: 120 of 432); MV_COMPACT=0 keeps them all.
 // Returns the genes to store (ascending), or empty when every gene is stored.
+static bool compact_allowed(const mv_engine* e) {
+  const char* env = std::getenv("MV_COMPACT");
+  return !(env && env[0] == '0') && e->p.ident && e->has_model;
+}
+
+// Gene g can never change in state b (the compact layout's rule, above).
+static bool gene_fixed(const HostProblem& h, int g, const double* x_init, const double* xl,
+                       const double* xu, int b) {
+  if (h.kind[g] != MV_GENE_INT) return false;
+  const int f = h.feat[g];
+  const double x = x_init[(size_t)b * h.D + f], lo = xl[(size_t)b * h.D + f],
+               hi = xu[(size_t)b * h.D + f];
+  return lo == hi && x == lo && std::rint(x) == x;
+}
+
 static std::vector<int> stored_genes(const mv_engine* e, int B, const double* x_init,
                                      const double* xl, const double* xu) {
   const HostProblem& h = e->hp;
   std::vector<int> keep;
-  const char* env = std::getenv("MV_COMPACT");
-  if ((env && env[0] == '0') || !e->p.ident || !e->has_model) return keep;
+  if (!compact_allowed(e)) return keep;
   for (int g = 0; g < h.V; ++g) {
-    bool fixed = h.kind[g] == MV_GENE_INT;
-    const int f = h.feat[g];
-    for (int b = 0; b < B && fixed; ++b) {
-      const double x = x_init[(size_t)b * h.D + f], lo = xl[(size_t)b * h.D + f],
-                   hi = xu[(size_t)b * h.D + f];
-      fixed = lo == hi && x == lo && std::rint(x) == x;
-    }
+    bool fixed = true;
+    for (int b = 0; b < B && fixed; ++b) fixed = gene_fixed(h, g, x_init, xl, xu, b);
     if (!fixed) keep.push_back(g);
   }
   if ((int)keep.size() == h.V || keep.empty()) keep.clear();
@@ -627,8 +657,26 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
                              (double*)e->s.gu, (unsigned char*)e->s.sblob, (float*)e->s.bias1,
                              e->genes0, (hipStream_t)stream));
   HIPCHK(release_rows(slot, (hipStream_t)stream));
-  // the attack's compact layout, when this state set has genes that never change
-  const std::vector<int> keep = stored_genes(e, B, x_init, xl, xu);
+  // the attack's compact layout, when this state set has genes that never change (or the
+  // layout mv_set_gene_layout requested, checked against this batch)
+  std::vector<int> keep;
+  if (e->layout_req.empty()) {
+    keep = stored_genes(e, B, x_init, xl, xu);
+  } else if (compact_allowed(e)) {
+    size_t j = 0;
+    for (int g = 0; g < e->hp.V; ++g) {
+      if (j < e->layout_req.size() && e->layout_req[j] == g) {
+        ++j;
+        continue;
+      }
+      for (int b = 0; b < B; ++b)
+        if (!gene_fixed(e->hp, g, x_init, xl, xu, b))
+          return fail(MV_ERR_ARG, "mv_set_gene_layout: gene " + std::to_string(g) +
+                                      " is not fixed in bound state " + std::to_string(b));
+    }
+    keep = e->layout_req;
+    if ((int)keep.size() == e->hp.V) keep.clear();
+  }
   if (!keep.empty()) {
     if (keep != e->stored) {
       HIPCHK(hipDeviceSynchronize());
@@ -672,6 +720,8 @@ static RowsArgs base_rows(const mv_engine* e, bool attack) {
 int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double* G, void* stream) {
   if (!e || n <= 0 || !genes || !F) return fail(MV_ERR_ARG, "bad mv_evaluate arguments");
   if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  if (!on_device(genes, e->device) || !on_device(F, e->device) || !on_device(G, e->device))
+    return fail(MV_ERR_ARG, "mv_evaluate: a buffer lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   RowsArgs a = base_rows(e);
   a.n = n;
@@ -694,6 +744,8 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
 int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* stream) {
   if (!e || n < 0 || (n > 0 && (!genes || !x))) return fail(MV_ERR_ARG, "bad mv_decode arguments");
   if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  if (!on_device(genes, e->device) || !on_device(x, e->device))
+    return fail(MV_ERR_ARG, "mv_decode: a buffer lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(launch_decode(e->p, e->s, e->B, n, genes, x, (hipStream_t)stream));
   return MV_OK;
@@ -701,6 +753,8 @@ int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* str
 
 int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream) {
   if (!e || n < 0 || (n > 0 && (!x || !G))) return fail(MV_ERR_ARG, "bad mv_constraints arguments");
+  if (!on_device(x, e->device) || !on_device(G, e->device))
+    return fail(MV_ERR_ARG, "mv_constraints: a buffer lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   int slot = 0;
   HIPCHK(stage_rows(base_rows(e), (hipStream_t)stream, &slot));
@@ -815,7 +869,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
                 "n_ref <= 640)");
   {
     const int n_m = (O + 1) / 2, pslots = ((n_m * 4 + P - 1) / P) * P;
-    if (surv_lds_bytes(P + O, R, pslots) > 160 * 1024)
+    const int ptab = plan_tab_words(e->ap().Vr, e->ap().V);
+    if (surv_lds_bytes(P + O, R, pslots, ptab) > 160 * 1024 ||
+        surv_lds_bytes(P, R, pslots, ptab) > 160 * 1024)
       return fail(MV_ERR_ARG, "pop_size + n_offsprings and n_ref too large for the survival LDS");
   }
   hipStream_t stream = (hipStream_t)stream_;
@@ -824,8 +880,18 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   const int B = e->B, V = ap.V, S = P + O;
   const int hist_w = prm->history == 2 ? 3 + ap.C : 3;
   const int hist_rows = P + (G - 1) * O;
+  // the offspring rows' kernel: k_genc reads a variation plan written by k_survive
+  bool use_plan = false;
+  {
+    RowsArgs t = base_rows(e, true);
+    t.n = O;
+    t.total = B * O;
+    t.mode = 1;
+    use_plan = row_kernel_kind(t) == 2;
+  }
   const bool realloc = !e->attack_ready || e->P != P || e->O != O || e->R != R ||
-                       e->hist_mode != prm->history || e->n_gen != G;
+                       e->hist_mode != prm->history || (prm->history && e->n_gen != G) ||
+                       e->has_plan != use_plan;  // the budget sizes the history only
   if (realloc) {
     HIPCHK(hipDeviceSynchronize());
     e->free_list(e->attack_allocs);
@@ -843,6 +909,15 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     A(&e->pop_slot, (size_t)B * P);
     A(&e->free_slot, (size_t)B * O);
     A(&e->parents, (size_t)B * O);
+    e->plan_hdr = nullptr;
+    e->plan_mw = nullptr;
+    e->plan_mu = nullptr;
+    if (use_plan) {
+      A(&e->plan_hdr, (size_t)B * O);
+      A(&e->plan_mw, (size_t)B * O * PLAN_MUT);
+      A(&e->plan_mu, (size_t)B * O * PLAN_MUT);
+    }
+    e->has_plan = use_plan;
     e->dom_g = nullptr;
     e->dom_stride = 0;
     if (S > SURV_NLDS) {
@@ -924,6 +999,11 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     if (r.genes_out) r.genes_out += b0 * r.out_rows * V;
     if (r.parents) r.parents += b0 * O;
     if (r.out_map) r.out_map += b0 * r.n;
+    if (r.plan_hdr) {
+      r.plan_hdr += b0 * O;
+      r.plan_mw += b0 * O * PLAN_MUT;
+      r.plan_mu += b0 * O * PLAN_MUT;
+    }
     if (r.F) r.F += b0 * r.out_rows * 3;
     if (r.hist) r.hist += b0 * (size_t)r.hist_rows * r.hist_w;
     // Each group owns xml rows [b0, b1) x max(P, O): one group's initial evaluation (n = P)
@@ -946,6 +1026,11 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     if (s.parents_out) s.parents_out += b0 * O;
     if (s.phase) s.phase += b0 * 32;
     if (s.dom_g) s.dom_g += b0 * s.dom_stride;
+    if (s.plan_hdr) {
+      s.plan_hdr += b0 * O;
+      s.plan_mw += b0 * O * PLAN_MUT;
+      s.plan_mu += b0 * O * PLAN_MUT;
+    }
     return s;
   };
   // initial population evaluation (pymoo _initialize)
@@ -982,6 +1067,21 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.O_next = O;
   sa.dom_g = e->dom_g;
   sa.dom_stride = e->dom_stride;
+  if (use_plan) {
+    const VaryOff vo = vary_offsets(ap);
+    sa.plan_hdr = e->plan_hdr;
+    sa.plan_mw = e->plan_mw;
+    sa.plan_mu = e->plan_mu;
+    sa.geo = (const uint32_t*)(ap.vblob + vo.geo);
+    sa.cmap = (const int*)(ap.vblob + vo.cmap);
+    sa.ginfo = (const int*)(ap.vblob + vo.ginfo);
+    sa.Vr = ap.Vr;
+    sa.V = ap.V;
+    sa.n_sub0 = ap.n_sub[0];
+    sa.n_sub1 = ap.n_sub[1];
+    sa.cx_prob = e->cx_prob;
+    sa.cx_sbx = e->cx_kind == 1;
+  }
   if (std::getenv("MV_SURV_PHASES")) {
     if (!e->d_phase) {
       HIPCHK(hipMalloc((void**)&e->d_phase, (size_t)B * 32 * sizeof(long long)));
@@ -1025,6 +1125,11 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   va.hist_w = hist_w;
   va.seed = prm->seed;
   va.xml = e->xml;
+  if (use_plan) {
+    va.plan_hdr = e->plan_hdr;
+    va.plan_mw = e->plan_mw;
+    va.plan_mu = e->plan_mu;
+  }
   const bool mlp_ph = std::getenv("MV_MLP_PHASES") != nullptr;
   if ((std::getenv("MV_GEN_PHASES") || mlp_ph) && ngrp == 1) {  // development: phase clocks
     const size_t n = (size_t)B * O * 16;  // >= grid * 16 (at least one row per workgroup)
@@ -1417,6 +1522,9 @@ int mv_objcalc_run(mv_objcalc* o, mv_engine* e, mv_mlp* m, int32_t B, int32_t n,
   if (!x_init || !x || !obj || !range_bad) return fail(MV_ERR_ARG, "null buffer");
   if (e->device != o->device || m->device != o->device)
     return fail(MV_ERR_ARG, "objects live on different devices");
+  if (!on_device(x_init, o->device) || !on_device(x, o->device) || !on_device(obj, o->device) ||
+      !on_device(range_bad, o->device))
+    return fail(MV_ERR_ARG, "mv_objcalc_run: a buffer lives on another device than the objects");
   hipStream_t stream = (hipStream_t)stream_;
   HIPCHK(hipSetDevice(o->device));
   HIPCHK(grow(&o->G, &o->cap_G, (size_t)total * (e->p.C > 0 ? e->p.C : 1)));
@@ -1534,6 +1642,32 @@ int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
                                     std::to_string(r[4]) + ", " + std::to_string(r[5]) +
                                     " failures)");
   }
+  return MV_OK;
+}
+
+int mv_gene_layout(mv_engine* e, int32_t B, const double* x_init, const double* xl,
+                   const double* xu, int32_t* stored, int32_t* n_stored) {
+  if (!e || B < 0 || (B > 0 && (!x_init || !xl || !xu)) || !stored || !n_stored)
+    return fail(MV_ERR_ARG, "bad mv_gene_layout arguments");
+  const std::vector<int> keep = B > 0 ? stored_genes(e, B, x_init, xl, xu) : std::vector<int>{};
+  for (int g = 0; g < e->hp.V; ++g) stored[g] = keep.empty() ? 1 : 0;
+  for (int g : keep) stored[g] = 1;
+  *n_stored = keep.empty() ? e->hp.V : (int32_t)keep.size();
+  return MV_OK;
+}
+
+int mv_set_gene_layout(mv_engine* e, const int32_t* stored, int32_t V) {
+  if (!e) return fail(MV_ERR_ARG, "null engine");
+  if (!stored) {
+    e->layout_req.clear();
+    return MV_OK;
+  }
+  if (V != e->hp.V) return fail(MV_ERR_ARG, "mv_set_gene_layout: V differs from the problem's");
+  std::vector<int> keep;
+  for (int g = 0; g < V; ++g)
+    if (stored[g]) keep.push_back(g);
+  if (keep.empty()) return fail(MV_ERR_ARG, "mv_set_gene_layout: no stored gene");
+  e->layout_req = keep;
   return MV_OK;
 }
 

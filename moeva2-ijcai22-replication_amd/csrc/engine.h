@@ -157,7 +157,29 @@ struct RowsArgs {
   float* xml;               // scratch [total][Dm4]: fp32 ML rows between k_vary and k_mlp
   long long* gphase;        // development (MV_GEN_PHASES): k_genc clocks [grid][8], or NULL
   long long* mphase;        // development (MV_MLP_PHASES): k_mlp2 clocks [grid][8]
+  // mode 1 under k_genc: the generation's variation plan, written by the previous k_survive
+  // (VPlan below); NULL: the row kernels draw the crossover / mutations themselves
+  const int4* plan_hdr;     // [B][n]
+  const int* plan_mw;       // [B][n][PLAN_MUT]
+  const double* plan_mu;    // [B][n][PLAN_MUT]
 };
+
+// Variation plan of one generation (k_survive's tail -> k_genc): every draw of the row
+// kernels' variation that does not depend on gene values, per offspring row i of a state
+// (mating m = i % (n / 2), side = i / (n / 2)):
+//   hdr  int4: x = parents packed (own | other << 16, pool slots), y / z = the real / int
+//        subsets' crossover draws (pack_cx: on | lo << 1 | hi << 16; SBX: on only),
+//        w = stored mutations count (<= PLAN_MUT) | overflow << 4 (the row has more: the row
+//        kernel redoes it with every mutation)
+//   mw   [PLAN_MUT] int: stored gene (bits 0-15) | real << 16 | from the other parent << 17
+//        (two-point: the gene lies in its subset's crossover segment)
+//   mu   [PLAN_MUT] double: the mutation's PM uniform
+// The draws are the ones the row kernels used to make (the same Philox indices and tags), so
+// the populations are bit-identical; only the gene value a mutation applies to, and its
+// det_pow, stay in the row kernel.
+constexpr int PLAN_MUT = 8;
+// k_survive stages the plan's tables in LDS: geo [Vr + 1], cmap [Vr], ginfo [V] words
+__host__ __device__ inline int plan_tab_words(int Vr, int V) { return 2 * Vr + 1 + V; }
 
 // Survival ------------------------------------------------------------------------------
 struct SurvArgs {
@@ -195,6 +217,17 @@ struct SurvArgs {
   long long* phase;         // [B][16] clock64() at phase boundaries (development), or NULL
   unsigned long long* dom_g;  // N > SURV_NLDS: dominance bitsets [B][dom_stride] in HBM
   size_t dom_stride;
+  // next generation's variation plan (RowsArgs VPlan), written after the tournament when
+  // plan_hdr != NULL: rows per state O_next, the attack layout's tables and crossover options
+  int4* plan_hdr;
+  int* plan_mw;
+  double* plan_mu;
+  const uint32_t* geo;      // [Vr + 1] geometric gap table (problem blob region B)
+  const int* cmap;          // [Vr] gene -> stored gene (-1 fixed)
+  const int* ginfo;         // [V] stored gene info (kind | subset index << 2 | ...)
+  int Vr, V, n_sub0, n_sub1;
+  double cx_prob;
+  int cx_sbx;               // SBX: the subsets' mating-level draws only
 };
 
 // Stand-alone classifier forward (Classifier.predict_proba) -------------------------------

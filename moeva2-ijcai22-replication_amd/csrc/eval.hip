@@ -124,6 +124,8 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   }
   preload();
   static_assert(CAP == 4, "row_draws maps 16 rows x 4 mutations onto the 64 lanes");
+  static_assert(VARY_ROWS_MAX <= 16 * VARY_W, "more than 16 rows per wave (vary_rows_per_wg)");
+  static_assert(VARY_ROWS_MAX <= (64 / PLAN_MUT) * VARY_W, "plan_draws: 8 rows per wave at most");
   const int lane = threadIdx.x & 63;
   const int kk = lane >> 2, qq = lane & 3;
   // (1) draw qq of row kk: its gap and PM uniform, then the positions (prefix sums of the
@@ -176,6 +178,50 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
   mut_v = cnt | ((int)((om >> (4 * (lane & 15) + 3)) & 1ull) << 3);
 }
 
+// The draws of a wave's rows from the generation's variation plan (k_genc; engine.h VPlan):
+// lane k < nrw holds row k's header (parents, crossover draws, mutation count | overflow
+// << 4), lane PLAN_MUT k + q row k's q-th planned mutation (pmw / pmu, loaded at kernel
+// start).  Two-point: the lane gathers the crossed parent's value at its stored gene and
+// mutates it (mutate_gene, as row_draws) -> mposv / mvalv; the first rows' parent loads go
+// out after the gathers, so the pow chains wait for the gathers only.  SBX: the mutations
+// apply to the row loop's SBX children, so mposv / mvalv keep the planned word / uniform.
+template <int NT, class Preload>
+__device__ __forceinline__ void plan_draws(const RowsArgs& a, const DProblem& p, const int b,
+                                           const bool mine, const bool sbx, const double* gin,
+                                           const int4 hdr, const int pmw, const double pmu,
+                                           int& par_v, int& cx0_v, int& cx1_v, int& mut_v,
+                                           int& mposv, double& mvalv, Preload&& preload) {
+  const int V = p.V;
+  if (mine) {
+    par_v = hdr.x;
+    cx0_v = hdr.y;
+    cx1_v = hdr.z;
+    mut_v = hdr.w;
+  }
+  const int lane = threadIdx.x & 63;
+  const int kk = lane >> 3, qq = lane & 7;
+  const int cnt = __shfl(mut_v, kk) & 15;  // rows past the wave's: mut_v 0
+  const bool hit = qq < cnt;
+  if (sbx) {
+    preload();
+    mposv = hit ? pmw : -1;
+    mvalv = pmu;
+    return;
+  }
+  const int park = __shfl(par_v, kk);
+  const int cq = hit ? MV_IDX(pmw & 0xFFFF, V, CK_GEN_MUTPOS) : 0;
+  const int mrow = MV_IDX(hit && ((pmw >> 17) & 1) ? (park >> 16) : (park & 0xFFFF), a.in_rows,
+                          CK_GEN_MUTROW);
+  const double* gl = a.s.gl + (size_t)b * V;
+  const double* gu = a.s.gu + (size_t)b * V;
+  double xv = gin[MV_IDX((size_t)mrow * V + cq, (long long)a.in_rows * V, CK_AT_MUTLOAD)];
+  const double lo = gl[MV_IDX(cq, V, CK_AT_BOUNDS)], hi = gu[MV_IDX(cq, V, CK_AT_BOUNDS)];
+  preload();
+  if (hit) xv = mutate_gene(xv, lo, hi, ((pmw >> 16) & 1) != 0, pmu, a.eta);
+  mposv = hit ? cq : -1;
+  mvalv = xv;
+}
+
 // k_gen: variation (mode 1) or gene load (mode 0), the child genes to the pool, the fp32
 // ML-scaled mutable row for k_mlp (default_problem.py:119-121) and f2, the encoder-MinMax
 // distance (default_problem.py:80-91).
@@ -188,9 +234,13 @@ __device__ __forceinline__ void row_draws(const RowsArgs& a, const DProblem& p, 
 // gene), at most MUT_CAP per row cached in registers, the rare rest finished in the row.
 // SBX: the SBX crossover option compiled in (a separate instance: its pow()-heavy path
 // doubled the two-point kernel's registers, halving its occupancy).
-template <bool IDENT, int NT, bool SBX>
+// PLAN (k_genc): mode 1 takes its draws from the variation plan (plan_draws).  EARLY (k_genc's
+// two-point slim instance, IDENT): the whole kernel's LDS is staged here (genc_early_lds) and
+// phase 1 reads its gene tables from the problem blob.
+template <bool IDENT, int NT, bool SBX, bool PLAN = false, bool EARLY = false>
 __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
                                         unsigned char* smem) {
+  static_assert(!EARLY || (IDENT && PLAN && !SBX), "early staging: k_genc two-point only");
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -199,29 +249,55 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const int V = p.V, Dm = p.Dm, Dm4 = p.Dm4;
   const bool ev = a.do_eval != 0;
   const VaryOff o = vary_offsets(p);
-  const GenLds L = gen_lds(o, REGC, IDENT, ev);
+  const GenLds L = EARLY ? genc_early_lds(o, p) : gen_lds(o, REGC, IDENT, ev);
   const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
   // the rows' matings and destinations first: their round trips (the parents come from the
   // previous k_survive) overlap the LDS staging instead of following it
   const bool mine = lane < nrw;
   const int irow = rc.i0 + wave + VARY_W * lane;
   int2 pre_pr = make_int2(0, 0);
+  int4 phdr = make_int4(0, 0, 0, 0);
+  int pmw = 0;
+  double pmu = 0.0;
   int orow_v = 0;
+  if (PLAN && a.mode == 1) {  // lane PLAN_MUT k + q: row k's q-th planned mutation
+    const int ir = min(rc.i0 + wave + VARY_W * (lane / PLAN_MUT), a.n - 1);
+    const size_t e = ((size_t)b * a.n + ir) * PLAN_MUT + (lane % PLAN_MUT);
+    pmw = a.plan_mw[e];
+    pmu = a.plan_mu[e];
+  }
   if (mine) {
     if (a.mode == 1) {
-      const int nm = a.n / 2;
-      pre_pr = *(const int2*)(a.parents + ((size_t)b * nm + irow % nm) * 2);
-      pre_pr.x = MV_IDX(pre_pr.x, a.in_rows, CK_GEN_PARENT);
-      pre_pr.y = MV_IDX(pre_pr.y, a.in_rows, CK_GEN_PARENT);
+      if (PLAN) {
+        phdr = a.plan_hdr[(size_t)b * a.n + irow];
+        const int pa = MV_IDX(phdr.x & 0xFFFF, a.in_rows, CK_GEN_PARENT);
+        const int pb = MV_IDX(phdr.x >> 16, a.in_rows, CK_GEN_PARENT);
+        phdr.x = pa | (pb << 16);
+      } else {
+        const int nm = a.n / 2;
+        pre_pr = *(const int2*)(a.parents + ((size_t)b * nm + irow % nm) * 2);
+        pre_pr.x = MV_IDX(pre_pr.x, a.in_rows, CK_GEN_PARENT);
+        pre_pr.y = MV_IDX(pre_pr.y, a.in_rows, CK_GEN_PARENT);
+      }
     }
     orow_v = MV_IDX(a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow, a.out_rows, CK_GEN_DST);
   }
-  glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
-  if (ev && !REGC) {
-    glds_copy(smem + L.c_at, p.vblob + o.c_at, o.c_end - o.c_at, wave, lane);
-    glds_copy(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
+  if (EARLY) {  // phase 2's program + x_init, phase 1's encoder (and scaler) coefficients
+    const unsigned ssz = o.s_end - o.s_at;
+    glds_copy(smem, p.vblob + o.s_at, ssz, wave, lane);
+    glds_copy(smem + ssz, sblob, o.x_end, wave, lane);
+    if (ev) {
+      glds_copy(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
+      if (!p.xml_direct) glds_copy(smem + L.c_at, p.vblob + o.c_at, o.c_end - o.c_at, wave, lane);
+    }
+  } else {
+    glds_copy(smem + L.b_at, p.vblob + o.b_at, o.b_end - o.b_at, wave, lane);
+    if (ev && !REGC) {
+      glds_copy(smem + L.c_at, p.vblob + o.c_at, o.c_end - o.c_at, wave, lane);
+      glds_copy(smem + L.e_at, sblob + o.e_at, o.sb - o.e_at, wave, lane);
+    }
+    if (ev && !IDENT) glds_copy(smem + L.x_at, sblob, o.x_end, wave, lane);
   }
-  if (ev && !IDENT) glds_copy(smem + L.x_at, sblob, o.x_end, wave, lane);
   // per-lane gene-table words and (REGC) coefficients, straight from HBM meanwhile
   int ginf[NT];
   double cS[NT], cM[NT], cE[NT], cN[NT], cX[NT];
@@ -250,11 +326,13 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 1] = clock64();
-  const int* s_ginfo = (const int*)(smem + L.b_at + (o.ginfo - o.b_at));
-  const uint32_t* s_geo = (const uint32_t*)(smem + L.b_at + (o.geo - o.b_at));
-  const int* s_mutf = (const int*)(smem + L.b_at + (o.mutf - o.b_at));
-  const int* s_cmap = (const int*)(smem + L.b_at + (o.cmap - o.b_at));
-  const int* s_fidx = (const int*)(smem + L.b_at + (o.fidx - o.b_at));
+  // region B: LDS, or (EARLY) the problem blob itself (only the rare overflow rows read it)
+  const unsigned char* rb_ = EARLY ? p.vblob + o.b_at : smem + L.b_at;
+  const int* s_ginfo = (const int*)(rb_ + (o.ginfo - o.b_at));
+  const uint32_t* s_geo = (const uint32_t*)(rb_ + (o.geo - o.b_at));
+  const int* s_mutf = (const int*)(rb_ + (o.mutf - o.b_at));
+  const int* s_cmap = (const int*)(rb_ + (o.cmap - o.b_at));
+  const int* s_fidx = (const int*)(rb_ + (o.fidx - o.b_at));
   const double* s_mlS = (const double*)(smem + L.c_at + (o.mlS - o.c_at));
   const double* s_mlM = (const double*)(smem + L.c_at + (o.mlM - o.c_at));
   const double* s_es = (const double*)(smem + L.e_at + (o.es - o.e_at));
@@ -291,8 +369,12 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (nrw > 1) load_row(1, xb);
   };
   if (a.mode == 1) {
-    row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, s_cmap, gin, rng, par_v,
-                       cx0_v, cx1_v, mut_v, mposv, mvalv, pre_pr, preload);
+    if constexpr (PLAN)
+      plan_draws<NT>(a, p, b, mine, sbx, gin, phdr, pmw, pmu, par_v, cx0_v, cx1_v, mut_v, mposv,
+                     mvalv, preload);
+    else
+      row_draws<MUT_CAP>(a, p, b, irow, mine, gen, sbx, s_geo, s_ginfo, s_cmap, gin, rng, par_v,
+                         cx0_v, cx1_v, mut_v, mposv, mvalv, pre_pr, preload);
   } else {
     if (mine) par_v = irow | (irow << 16);
     preload();
@@ -383,15 +465,23 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       sbx_row<NT>(x, ginf, gin + (size_t)(pr & 0xFFFF) * V, gin + (size_t)(pr >> 16) * V, sgl,
                   sgu, V, s_fidx, i % nm, i / nm, rdl(cx0_v, k) & 1, rdl(cx1_v, k) & 1, rng, gen,
                   a.sbx_eta, lane, (int*)(sb + 64 * NT * 8), (double*)sb);
-      mutate_row_full<NT>(x, s_geo, s_ginfo, s_cmap, sgl, sgu, p.Vr, i, rng, gen, a.eta, lane);
+      const int mv = rdl(mut_v, k);
+      if (PLAN && !(mv & 16))
+        plan_mutate_row<NT>(x, mv & 15, mposv, mvalv, k, lane, sgl, sgu, V, a.eta);
+      else  // every mutation of the row (PLAN: more than PLAN_MUT)
+        mutate_row_full<NT>(x, s_geo, s_ginfo, s_cmap, sgl, sgu, p.Vr, i, rng, gen, a.eta, lane);
     } else if (a.mode == 1) {  // apply the row's cached mutations
-      apply_row_mutations<NT, MUT_CAP>(x, rdl(mut_v, k) & 7, mposv, mvalv, k, lane);
+      if constexpr (PLAN)
+        apply_row_mutations<NT, PLAN_MUT>(x, rdl(mut_v, k) & 15, mposv, mvalv, k, lane);
+      else
+        apply_row_mutations<NT, MUT_CAP>(x, rdl(mut_v, k) & 7, mposv, mvalv, k, lane);
     }
     finish_row(k, x);
   }
   // Rare: rows with more than MUT_CAP mutations are redone here with every mutation (same
   // lanes, same addresses, so these stores land after the row loop's).
-  if (a.mode == 1 && __ballot(mut_v & 8)) {
+  constexpr int OVF = PLAN ? 16 : 8;  // more mutations than the plan / the register cache
+  if (a.mode == 1 && !sbx && __ballot(mut_v & OVF)) {
     const RowsArgs* ap = &a;
     const uint64_t seed2 = *(volatile const uint64_t*)&ap->seed;
     const Rng rng2(seed2, state_stream(a.stream_key, a.state_keys, a.key0, b));
@@ -400,7 +490,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     const int Vr = p.Vr;
     const float lq = __log2f(1.0f - 1.0f / (float)Vr);
     for (int k = 0; k < nrw; ++k) {
-      if (!(rdl(mut_v, k) & 8)) continue;
+      if (!(rdl(mut_v, k) & OVF)) continue;
       const int i = rc.i0 + wave + VARY_W * k;
       double x[NT];
       load_row(k, x);
@@ -442,10 +532,13 @@ __global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0
 // evaluates its (register-packed) ops.
 // SLIM (k_genc, DProblem.slim): region S staged instead of region A, the lane ops' packed
 // words loaded straight from the problem blob (see kernels.h).
-template <bool FULL, bool IDENT, int NT, bool SLIM = false>
+// STAGED (k_genc's early-staged instance): regions S and X are already in LDS, behind the
+// k_genc phase barrier.
+template <bool FULL, bool IDENT, int NT, bool SLIM = false, bool STAGED = false>
 __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int rows_wg,
                                           unsigned char* smem, bool have_dst = false,
                                           int dst_pre = 0) {
+  static_assert(!STAGED || SLIM, "early staging: the slim program only");
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
@@ -493,11 +586,11 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
       const unsigned w = gw[c < n_lane ? c : 0];
       opw[k] = (k < kops && c < n_lane) ? w : 0u;
     }
-    glds_copy<CONS_T>(smem, p.vblob + o.s_at, pa, wave, lane);
+    if (!STAGED) glds_copy<CONS_T>(smem, p.vblob + o.s_at, pa, wave, lane);
   } else {
     glds_copy<CONS_T>(smem, p.vblob, pa, wave, lane);
   }
-  glds_copy<CONS_T>(smem + pa, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
+  if (!STAGED) glds_copy<CONS_T>(smem + pa, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
   int ginf[NT];
   {
     const int* gi = (const int*)(p.vblob + o.ginfo);
@@ -508,8 +601,10 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
       ginf[t] = g < V ? w : 0;
     }
   }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
+  if (!STAGED) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
   if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
   double* xrow = (double*)(smem + pa + o.x_end + wave * (SLIM ? o.rbs : o.rb));
   const double* s_xi = (const double*)(smem + pa + o.xi);
@@ -635,14 +730,15 @@ __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows
     a.gphase[(size_t)blockIdx.x * 8 + 0] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 6] = wall_clock64();
   }
-  const int orow_v = gen_rows<IDENT, NT, SBX>(a, gen, hist_row0, rows_wg, smem);
+  constexpr bool EARLY = SLIM && !SBX;  // the whole LDS staged at the start (genc_early_lds)
+  const int orow_v = gen_rows<IDENT, NT, SBX, true, EARLY>(a, gen, hist_row0, rows_wg, smem);
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) a.gphase[(size_t)blockIdx.x * 8 + 3] = clock64();
   // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
   // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them.  Both
   // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  cons_rows<false, IDENT, NT, SLIM>(a, hist_row0, rows_wg, smem, true, orow_v);
+  cons_rows<false, IDENT, NT, SLIM, EARLY>(a, hist_row0, rows_wg, smem, true, orow_v);
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 7] = wall_clock64();
@@ -1749,8 +1845,11 @@ static void allow_lds(K kern) {
 static int vary_rows_per_wg(int n) {
   static const char* env = std::getenv("MV_VARY_ROWS");
   static int cap = [] {
+    // row_draws maps a wave's rows onto lanes 4 k + q, plan_draws onto PLAN_MUT k + q: at
+    // most 64 / PLAN_MUT rows per wave
+    constexpr int hi = (64 / PLAN_MUT) * VARY_W < 64 ? (64 / PLAN_MUT) * VARY_W : 64;
     const int v = env ? std::atoi(env) : VARY_ROWS_MAX;
-    return v < 4 ? 4 : (v > 64 ? 64 : v);
+    return v < 4 ? 4 : (v > hi ? hi : v);
   }();
   const int c0 = (n + cap - 1) / cap;
   if (env) return (n + c0 - 1) / c0;
@@ -1899,7 +1998,9 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const bool slim = a.p.slim != 0;
     const size_t lc = slim ? cons_lds_slim(o) : cons_lds_total(o);
     static const size_t pad = lds_pad("MV_LDS_PAD_GENC");
-    const size_t lds = (lg > lc ? lg : lc) + pad;
+    const size_t lds = (slim && !sbx ? genc_early_lds(o, a.p).total : (lg > lc ? lg : lc)) + pad;
+    // k_genc takes mode 1's draws from the variation plan (mv_attack_run's k_survive)
+    if (a.mode == 1 && !(a.plan_hdr && a.plan_mw && a.plan_mu)) return hipErrorInvalidValue;
     if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
     if (nt == 5) return genc_go<5>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
     if (nt == 6) return genc_go<6>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);

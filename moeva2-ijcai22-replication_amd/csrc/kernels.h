@@ -130,6 +130,25 @@ __host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool iden
   l.total = at;
   return l;
 }
+// k_genc's two-point slim instance stages everything at its start: phase 2's region S and X
+// at 0, and phase 1's region E (and C unless xml_direct) in the space of phase 2's row
+// buffers, which are written only after the phase barrier (so no staging sits between the
+// phases).  Phase 1 reads its gene tables from the problem blob (the variation plan leaves
+// only the gene info there).
+__host__ __device__ inline GenLds genc_early_lds(const VaryOff& o, const DProblem& p) {
+  GenLds l{};
+  const unsigned rows_at = (o.s_end - o.s_at) + o.x_end;
+  const unsigned e_sz = o.sb - o.e_at;
+  l.b_at = 0;
+  l.e_at = rows_at;
+  l.c_at = rows_at + e_sz;
+  l.x_at = o.s_end - o.s_at;
+  l.rows_at = rows_at;
+  const unsigned ph1 = e_sz + (p.xml_direct ? 0u : (o.c_end - o.c_at));
+  const unsigned ph2 = CONS_W * o.rbs;
+  l.total = rows_at + (ph1 > ph2 ? ph1 : ph2);
+  return l;
+}
 // SBX rows: a per-wave list of the crossed genes (int) and their children (double) after the
 // k_gen layout (rowops.h sbx_row)
 __host__ __device__ inline unsigned gen_sbx_at(const GenLds& l) { return (l.total + 15u) & ~15u; }
@@ -172,7 +191,7 @@ hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, cons
 // the returned slot, then release it on the same stream after the slot's last launch.
 hipError_t stage_rows(const RowsArgs& a, hipStream_t stream, int* slot);
 hipError_t release_rows(int slot, hipStream_t stream);
-size_t surv_lds_bytes(int N, int R, int P);
+size_t surv_lds_bytes(int N, int R, int P, int ptab_words = 0);
 
 hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream);
 // Which kernels launch_gen / launch_cons run for these rows: 0 k_gen + k_cons, 1 k_narrow

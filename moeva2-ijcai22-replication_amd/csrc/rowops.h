@@ -3,6 +3,7 @@
 #pragma once
 #include "check.h"
 #include "detmath.h"
+#include "draws.h"
 #include "engine.h"
 #include "kernels.h"
 #include "philox.h"
@@ -261,31 +262,6 @@ __device__ __forceinline__ double poly_mut(double x, double xl, double xu, doubl
   return y;
 }
 
-// Crossover draws of one mating for one variable-type subset (oracle crossover_draws):
-// on = u53 < prob; genes of the subset with index in [lo, hi) are swapped.
-struct CxSub {
-  int on, lo, hi;
-};
-
-__device__ __forceinline__ CxSub cx_sub(const Rng& rng, int gen, int m, int s, int n,
-                                        double prob) {
-  CxSub c{0, 0, 0};
-  if (n <= 0) return c;
-  const u32x4 w = rng.draw((uint32_t)(m * 2 + s), (uint32_t)gen, TAG_CX);
-  c.on = u53(w.x, w.y) < prob;
-  if (n - 1 <= 0) return c;
-  const int a = 1 + (int)(((uint64_t)w.z * (uint64_t)(n - 1)) >> 32);
-  if (n - 1 == 1) {
-    c.lo = a;
-    c.hi = n;
-  } else {
-    int b = 1 + (int)(((uint64_t)w.w * (uint64_t)(n - 2)) >> 32);
-    if (b >= a) ++b;
-    c.lo = a < b ? a : b;
-    c.hi = a < b ? b : a;
-  }
-  return c;
-}
 
 __device__ __forceinline__ void scatter_gene(const DProblem& p, double* __restrict__ xrow,
                                              int info, double x) {
@@ -315,17 +291,6 @@ __device__ __forceinline__ void scatter_gene_tab(const int* __restrict__ ooff,
 
 __device__ __forceinline__ int rdl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
-// Geometric gap of the mutation process (oracle mutation_draws): the number of
-// non-mutated genes before the next mutated one is the largest k in [0, V] with
-// w < T[k], T[k] = floor((1 - 1/V)^k * 2^32) (T[0] unused), found by binary search.
-__device__ __forceinline__ int geo_gap(const uint32_t* T, int V, uint32_t w, float lq) {
-  // estimate from log2(w / 2^32) / log2(1 - 1/V), then step to the exact table answer
-  int k = (int)(__log2f(((float)w + 0.5f) * 2.3283064365386963e-10f) / lq);
-  k = k < 0 ? 0 : (k > V ? V : k);
-  while (k < V && w < T[k + 1]) ++k;
-  while (k > 0 && !(w < T[k])) --k;
-  return k;
-}
 
 // pymoo 0.4.2.2 SimulatedBinaryCrossover._do for one gene of one mating [pymoo-recall;
 // SURVEY.md §7 "north_star says SBX"]: the child of `side` (0: c[0], 1: c[1]) from parents
@@ -365,7 +330,6 @@ __device__ __forceinline__ double mutate_gene(double x, double xl, double xu, bo
 }
 
 constexpr int MUT_CAP = 4;     // mutations per row precomputed in the prologue (registers)
-constexpr int MUT_J = 1024;    // Philox indices per row of the mutation stream (V <= 1024)
 
 // SBX option of the mixed-variable crossover (real_sbx / int_sbx = IntegerFromFloat-
 // Crossover(SBX): widened bounds, np.round, then the build's clamp to [xl, xu]) for one row
@@ -469,13 +433,6 @@ __device__ __forceinline__ bool gene_swapped(int info, int on0, int lo0, int hi0
 }
 
 
-// Crossover draws of one subset packed into one word: on | lo << 1 | hi << 16.
-__device__ __forceinline__ int pack_cx(const CxSub& c) { return c.on | (c.lo << 1) | (c.hi << 16); }
-__device__ __forceinline__ bool swapped_packed(int info, int cx0, int cx1) {
-  const int sub = (info >> 2) & 0x7FFF;
-  const int c = (info & 3) == 0 ? cx0 : cx1;
-  return (c & 1) && sub >= ((c >> 1) & 0x7FFF) && sub < (c >> 16);
-}
 __device__ __forceinline__ double rdl_d(double v, int k) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
@@ -728,15 +685,40 @@ __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, int mpo
                                                     int k, int lane) {
 #pragma unroll
   for (int q = 0; q < CAP; ++q) {
-    const int pr = rdl(mposv, 4 * k + q);  // stored gene; -1: a fixed gene (compact layout)
+    const int pr = rdl(mposv, CAP * k + q);  // stored gene; -1: a fixed gene (compact layout)
     if (q < nmut && pr >= 0) {
       const int pos = MV_IDX(pr, 64 * NT, CK_GEN_APPLY);
-      const double y = rdl_d(mvalv, 4 * k + q);
+      const double y = rdl_d(mvalv, CAP * k + q);
       const int tt = pos >> 6;
       const bool me = lane == (pos & 63);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         if (t == tt) x[t] = me ? y : x[t];
+    }
+  }
+}
+
+// The planned mutations of an SBX row k (lane PLAN_MUT k + q: mw word, PM uniform), applied
+// to the row's SBX children: the gene's lane mutates it (the order of distinct positions does
+// not matter).
+template <int NT>
+__device__ __forceinline__ void plan_mutate_row(double* x, int nmut, int mwv, double muv, int k,
+                                                int lane, const double* gl, const double* gu,
+                                                int V, double eta) {
+  for (int q = 0; q < nmut; ++q) {
+    const int w = rdl(mwv, PLAN_MUT * k + q);
+    const double u = rdl_d(muv, PLAN_MUT * k + q);
+    const int cq = MV_IDX(w & 0xFFFF, V, CK_GEN_APPLY);
+    const int tt = cq >> 6;
+    if (lane == (cq & 63)) {
+      double xv = 0.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t == tt) xv = x[t];
+      xv = mutate_gene(xv, gl[cq], gu[cq], ((w >> 16) & 1) != 0, u, eta);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t == tt) x[t] = xv;
     }
   }
 }

@@ -19,6 +19,7 @@
 #include <limits.h>
 
 #include "check.h"
+#include "draws.h"
 #include "engine.h"
 #ifdef MV_CHECKS
 namespace mv {
@@ -106,7 +107,7 @@ constexpr int NICHE_SORT_MIN = 256;
 struct SurvOff {
   unsigned F, ref, U, Uf, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
       key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm,
-      dmin, lround, total;
+      dmin, lround, ptab, total;
 };
 
 // Niching's temporaries (count, remain, csr_off, csr, cand, ckey, dmin, lround) are dead
@@ -114,7 +115,10 @@ struct SurvOff {
 // (N <= SURV_NLDS) and the temporaries fit inside them they share those bytes; the
 // reference points are read from global memory (L2-resident, the same for every state).
 // Round 4: 68.8 -> ~53 KiB per workgroup at N = 303, R = 200 (three workgroups per CU).
-__host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm) {
+// ptab_words: the variation plan's tables (geo, cmap, ginfo; 0 without a plan), staged after
+// survivor selection into the F rows when they fit (F is dead then), else appended.
+__host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm,
+                                                         int ptab_words = 0) {
   const bool dom_lds = N <= SURV_NLDS;
   const unsigned NW = (N + 63) / 64;
   const unsigned RN = R + 3;
@@ -167,10 +171,19 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(ckey, RN * 4)
   TAKE(dmin, (size_t)RN * 8)
   TAKE(lround, (size_t)(2 * N + 2) * 4)
+  unsigned total = alias ? end : off;
+  if (ptab_words > 0 && (size_t)ptab_words * 4 > (size_t)NW * 64 * 3 * 8) {
+    off = total;
+    TAKE(ptab, (size_t)ptab_words * 4)
+    total = off;
+  } else {
+    o.ptab = o.F;
+  }
 #undef TAKE
-  o.total = alias ? end : off;
+  o.total = total;
   return o;
 }
+
 
 __device__ __forceinline__ double min_prop(double a, double b) {  // np.min (NaN propagates)
   double r = b < a ? b : a;
@@ -293,7 +306,7 @@ __device__ inline bool lu_solve3(double A[3][3], double x[3]) {
 template <int T>
 __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uint32_t sk, int gen,
                            const int* map_slot, int* out, unsigned long long* sortk,
-                           int* perm) {
+                           int* perm, int* lds_out = nullptr) {
   const int tid = threadIdx.x;
   const int n_m = (O_next + 1) / 2;
   const int n_random = n_m * 4;
@@ -324,7 +337,56 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
     const int a = perm[2 * t], b = perm[2 * t + 1];
     const unsigned bit = rng.draw((uint32_t)t, (uint32_t)gen, TAG_SEL_CHOICE).x & 1u;
     const int w = bit ? b : a;
-    out[t] = map_slot ? map_slot[MV_IDX(w, P, CK_SURV_PARENT)] : w;
+    const int v = map_slot ? map_slot[MV_IDX(w, P, CK_SURV_PARENT)] : w;
+    out[t] = v;
+    if (lds_out) lds_out[t] = v;  // the sort keys are dead after the rank pass's barrier
+  }
+}
+
+// The next generation's variation plan (engine.h VPlan) of state b: thread i < O_next takes
+// offspring row i -- its parents from the tournament (par: LDS, 2 per mating), the two
+// crossover subsets' draws (rowops cx_sub, as row_draws), and its mutations: the same
+// geometric-gap walk over the Vr genes as the row kernels (Philox index i * MUT_J + j,
+// TAG_MUT_MASK), positions mapped to stored genes (a fixed gene's draw is consumed, nothing
+// is written), at most PLAN_MUT kept (more: the overflow flag).  geo / cmap / ginfo: LDS.
+template <int T>
+__device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, const int gen,
+                                               const int* par, const uint32_t* geo,
+                                               const int* cmap, const int* ginfo) {
+  const int n = a.O_next, nm = n / 2;
+  const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
+  const int Vr = a.Vr;
+  const float lq = __log2f(1.0f - 1.0f / (float)Vr);
+  for (int i = threadIdx.x; i < n; i += T) {
+    const int m = i % nm, side = i / nm;
+    const int p0 = par[2 * m], p1 = par[2 * m + 1];
+    const int pv = side ? (p1 | (p0 << 16)) : (p0 | (p1 << 16));
+    int c0 = pack_cx(cx_sub(rng, gen, m, 0, a.n_sub0, a.cx_prob));
+    int c1 = pack_cx(cx_sub(rng, gen, m, 1, a.n_sub1, a.cx_prob));
+    if (a.cx_sbx) {
+      c0 &= 1;
+      c1 &= 1;
+    }
+    int* mw = a.plan_mw + ((size_t)b * n + i) * PLAN_MUT;
+    double* mu = a.plan_mu + ((size_t)b * n + i) * PLAN_MUT;
+    int cnt = 0, ovf = 0, pos = -1;
+    for (int j = 0;; ++j) {
+      const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+      pos += 1 + geo_gap(geo, Vr, w.x, lq);
+      if (pos >= Vr) break;
+      const int cq = cmap[pos];
+      if (cq < 0) continue;  // a fixed gene of the compact layout: its mutation is the identity
+      if (cnt == PLAN_MUT) {
+        ovf = 1;
+        break;
+      }
+      const int gi = ginfo[MV_IDX(cq, a.V, CK_GEN_MUTPOS)];
+      const int oth = (!a.cx_sbx && swapped_packed(gi, c0, c1)) ? 1 : 0;
+      mw[cnt] = cq | (((gi & 3) == 0 ? 1 : 0) << 16) | (oth << 17);
+      mu[cnt] = u53(w.y, w.z);
+      ++cnt;
+    }
+    a.plan_hdr[(size_t)b * n + i] = make_int4(pv, c0, c1, cnt | (ovf << 4));
   }
 }
 
@@ -341,7 +403,8 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   const int NW = (N + 63) / 64;
   const int n_m_next = parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = parents_out ? ((n_m_next * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
-  const SurvOff o = surv_offsets(N, R, pslots);
+  const bool plan = parents_out && a.plan_hdr;
+  const SurvOff o = surv_offsets(N, R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0);
   SurvLds L;
   L.F = (double*)(smem + o.F);
   L.ref = a.ref;  // global (surv_offsets)
@@ -632,87 +695,112 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     }
     PHASE(21)
+    // One packed reduction for the three argmins and the front's worst point, ONE barrier,
+    // then every wave combines the eight waves' partials and solves the nadir itself (the
+    // same bits in every wave), so no thread waits for a single-thread step.  The ASF values
+    // are >= +0, +inf or NaN: np.argmin's order (first NaN, else smallest value, ties the
+    // smallest index) is the lexicographic minimum of (NaN ? -1 : value, index), i.e. a
+    // v_min_f64 reduction of the keys, then a min of the indices holding the minimum key.
+    // The worst point: max over the non-NaN values, NaN if any value is NaN (max_prop).
+    double kmin[3], wmx[3];
+    int imin[3];
+    unsigned nanw = 0u;
     for (int i = 0; i < 3; ++i) {
-      wave_argbest(bv[i], bi[i], [](double v, int i1, double w, int i2) {
-        return arg_better(v, i1, w, i2);
-      });
-      wf[i] = wred_max(wf[i]);
+      const double key = bv[i] != bv[i] ? -1.0 : bv[i];
+      kmin[i] = wave_reduce(key, [](double x, double y) { return __builtin_fmin(x, y); });
+      int ix = key == kmin[i] ? bi[i] : INT_MAX;
+      ix = min(ix, dpp_i32<0xB1>(ix));
+      ix = min(ix, dpp_i32<0x4E>(ix));
+      ix = min(ix, dpp_i32<0x141>(ix));
+      ix = min(ix, dpp_i32<0x140>(ix));
+      int i0, i1;
+      swap_i32<16>(ix, i0, i1);
+      ix = min(i0, i1);
+      swap_i32<32>(ix, i0, i1);
+      imin[i] = min(i0, i1);
+      const bool wn = wf[i] != wf[i];
+      nanw |= __ballot(wn) ? (1u << i) : 0u;
+      wmx[i] = wave_reduce(wn ? -__builtin_inf() : wf[i],
+                           [](double x, double y) { return __builtin_fmax(x, y); });
     }
-    __syncthreads();
     if (lane == 0)
       for (int i = 0; i < 3; ++i) {
-        L.red[wave * 16 + i] = bv[i];
-        L.red[wave * 16 + 3 + i] = (double)bi[i];
-        L.red[wave * 16 + 6 + i] = wf[i];
+        L.red[wave * 16 + i] = kmin[i];
+        L.red[wave * 16 + 3 + i] = (double)imin[i];
+        L.red[wave * 16 + 6 + i] = (nanw >> i) & 1u ? __builtin_nan("") : wmx[i];
       }
-    __syncthreads();
-    if (tid < 3) {  // one thread per objective: winner of the extreme-point argmin
-      {
-        const int i = tid;
-        double v = L.red[i];
-        int ix = (int)L.red[3 + i];
-        double w = L.red[6 + i];
-        for (int ww = 1; ww < T / 64; ++ww) {
-          const double ov = L.red[ww * 16 + i];
-          const int oi = (int)L.red[ww * 16 + 3 + i];
-          if (arg_better(ov, oi, v, ix)) {
-            v = ov;
-            ix = oi;
-          }
-          w = max_prop(w, L.red[ww * 16 + 6 + i]);
-        }
-        wfront[i] = w;
-        double row[3];
-        if (ix < ne) {
-          for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
-        } else if (ix < ne + n0) {
-          const int m = L.I[ix - ne];
-          for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
-        } else {
-          for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
-        }
-        for (int k = 0; k < 3; ++k) ext[i * 3 + k] = row[k];
-      }
-    }
     __syncthreads();
     PHASE(22)
-    if (tid == 0) {
-      // nadir (get_nadir_point with the call-site argument swap)
-      double M[3][3], plane[3] = {1.0, 1.0, 1.0};
-      for (int i = 0; i < 3; ++i)
-        for (int k = 0; k < 3; ++k) M[i][k] = ext[i * 3 + k] - ideal[k];
-      double Mc[3][3];
-      for (int i = 0; i < 3; ++i)
-        for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
-      bool ok = lu_solve3(Mc, plane);
-      double nd[3];
-      if (ok) {
-        double icp[3];
-        for (int k = 0; k < 3; ++k) {
-          icp[k] = 1.0 / plane[k];
-          nd[k] = ideal[k] + icp[k];
+    double ex[9], wfr[3];
+    for (int i = 0; i < 3; ++i) {
+      double v = L.red[i];
+      int ix = (int)L.red[3 + i];
+      double w = L.red[6 + i];
+      for (int ww = 1; ww < T / 64; ++ww) {
+        const double ov = L.red[ww * 16 + i];
+        const int oi = (int)L.red[ww * 16 + 3 + i];
+        if (ov < v || (ov == v && oi < ix)) {
+          v = ov;
+          ix = oi;
         }
-        bool close = true, small = false;
-        for (int i = 0; i < 3; ++i) {
-          const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
-          close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
-          small = small || (icp[i] <= 1e-6);
-        }
-        if (!close || small) {
-          ok = false;
-        } else {
-          for (int k = 0; k < 3; ++k)
-            if (nd[k] > worst[k]) nd[k] = worst[k];
-        }
+        w = max_prop(w, L.red[ww * 16 + 6 + i]);
       }
-      if (!ok)
-        for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
+      wfr[i] = w;
+      double row[3];
+      if (ix < ne) {
+        for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
+      } else if (ix < ne + n0) {
+        const int m = L.I[ix - ne];
+        for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
+      } else {
+        for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
+      }
+      for (int k = 0; k < 3; ++k) ex[i * 3 + k] = row[k];
+    }
+    // nadir (get_nadir_point with the call-site argument swap), in every wave
+    double idl[3];
+    for (int k = 0; k < 3; ++k) idl[k] = ideal[k];
+    double M[3][3], plane[3] = {1.0, 1.0, 1.0};
+    for (int i = 0; i < 3; ++i)
+      for (int k = 0; k < 3; ++k) M[i][k] = ex[i * 3 + k] - idl[k];
+    double Mc[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
+    bool ok = lu_solve3(Mc, plane);
+    double nd[3];
+    if (ok) {
+      double icp[3];
       for (int k = 0; k < 3; ++k) {
-        if (nd[k] - ideal[k] <= 1e-6) nd[k] = wfront[k];
+        icp[k] = 1.0 / plane[k];
+        nd[k] = idl[k] + icp[k];
+      }
+      bool close = true, small = false;
+      for (int i = 0; i < 3; ++i) {
+        const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
+        close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
+        small = small || (icp[i] <= 1e-6);
+      }
+      if (!close || small) {
+        ok = false;
+      } else {
+        for (int k = 0; k < 3; ++k)
+          if (nd[k] > worst[k]) nd[k] = worst[k];
+      }
+    }
+    if (!ok)
+      for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
+    for (int k = 0; k < 3; ++k)
+      if (nd[k] - idl[k] <= 1e-6) nd[k] = wfr[k];
+    // every wave writes the same values; each wave reads back only what it wrote itself
+    // (LDS is in order within a wave) until the next barrier
+    if (lane == 0) {
+      for (int k = 0; k < 9; ++k) ext[k] = ex[k];
+      for (int k = 0; k < 3; ++k) {
+        wfront[k] = wfr[k];
         nadir[k] = nd[k];
       }
     }
-    __syncthreads();
+    wave_sync();
   }
   PHASE(4)
 
@@ -1132,6 +1220,18 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   }
   __syncthreads();
   PHASE(7)
+  // the variation plan's tables, into the (now dead) F rows: their loads overlap the outputs
+  uint32_t* pgeo = (uint32_t*)(smem + o.ptab);
+  int* pcmap = (int*)(pgeo + a.Vr + 1);
+  int* pginfo = pcmap + a.Vr;
+  if (plan) {
+    const int nw = plan_tab_words(a.Vr, a.V);
+    for (int k = tid; k < nw; k += T) {
+      const int v = k <= a.Vr ? (int)a.geo[k]
+                              : (k < 2 * a.Vr + 1 ? a.cmap[k - a.Vr - 1] : a.ginfo[k - 2 * a.Vr - 1]);
+      pgeo[k] = (uint32_t)v;
+    }
+  }
 
   // ---- outputs
   for (int k = tid; k < N; k += T) L.memb[k] = 0;  // selected flags by merged index
@@ -1206,9 +1306,14 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   if (parents_out) {
     tournament<T>(a.n_survive, a.O_next, a.seed,
                   state_stream(a.stream_key, a.state_keys, a.key0, b), sel_gen, slot_mode ? L.sel : nullptr,
-               parents_out + (size_t)b * n_m_next * 2, L.sortk, L.perm);
+               parents_out + (size_t)b * n_m_next * 2, L.sortk, L.perm,
+               plan ? (int*)L.sortk : nullptr);
   }
   __syncthreads();
+  if (plan) {
+    variation_plan<T>(a, b, sel_gen, (const int*)L.sortk, pgeo, pcmap, pginfo);
+    __syncthreads();
+  }
   PHASE(9)
 #undef PHASE
 }

@@ -82,14 +82,17 @@ hipError_t take_survival_dump(double* out) {
 #endif
 }
 
-size_t surv_lds_bytes(int N, int R, int Pperm) { return surv_offsets(N, R, Pperm).total; }
+size_t surv_lds_bytes(int N, int R, int Pperm, int ptab_words) {
+  return surv_offsets(N, R, Pperm, ptab_words).total;
+}
 
 hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   const int n_m = a.parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = a.parents_out ? ((n_m * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
   static const size_t pad = lds_pad("MV_LDS_PAD_SURV");
-  const size_t lds = surv_lds_bytes(a.N, a.R, pslots) + pad;
+  const size_t lds =
+      surv_lds_bytes(a.N, a.R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0) + pad;
   static bool configured = false;
   if (!configured) {
     (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64>,

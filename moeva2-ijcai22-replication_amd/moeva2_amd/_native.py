@@ -30,7 +30,7 @@ EXPORTED = [
     "mv_get_attack_time", "mv_mlp_create", "mv_mlp_destroy",
     "mv_mlp_predict", "mv_objcalc_create", "mv_objcalc_destroy", "mv_objcalc_run",
     "mv_objcalc_score", "mv_det_pow", "mv_debug_checks", "mv_set_state_streams",
-    "mv_debug_survival_dump", "mv_get_stored_genes",
+    "mv_debug_survival_dump", "mv_get_stored_genes", "mv_gene_layout", "mv_set_gene_layout",
 ]
 
 _i32p = C.POINTER(C.c_int32)
@@ -119,6 +119,8 @@ def lib():
             "mv_set_state_streams": [vp, C.c_int32, C.c_int64],
             "mv_debug_survival_dump": [_f64p],
             "mv_get_stored_genes": [vp, _i32p, _i32p],
+            "mv_gene_layout": [vp, C.c_int32, _f64p, _f64p, _f64p, _i32p, _i32p],
+            "mv_set_gene_layout": [vp, _i32p, C.c_int32],
         }
         for name, args in sig.items():
             fn = getattr(L, name)
@@ -359,6 +361,26 @@ class Engine:
         n = C.c_int32(0)
         check(lib().mv_get_stored_genes(self._h, st.ctypes.data_as(_i32p), C.byref(n)))
         return st.astype(bool)
+
+    def gene_layout(self, x_init, xl, xu) -> np.ndarray:
+        """The layout mv_set_states would derive for these states (mv_gene_layout; host
+        computation): bool [V], True = stored."""
+        x_init, xl, xu = (_arr(a, np.float64) for a in (x_init, xl, xu))
+        st = np.zeros(self.prog.V, np.int32)
+        n = C.c_int32(0)
+        check(lib().mv_gene_layout(self._h, x_init.shape[0], x_init.ctypes.data_as(_f64p),
+                                   xl.ctypes.data_as(_f64p), xu.ctypes.data_as(_f64p),
+                                   st.ctypes.data_as(_i32p), C.byref(n)))
+        return st.astype(bool)
+
+    def set_gene_layout(self, stored=None):
+        """Fix the layout of the next set_states calls (mv_set_gene_layout): bool [V] as
+        gene_layout returned it for the whole job, or None to derive it per bound batch."""
+        if stored is None:
+            check(lib().mv_set_gene_layout(self._h, None, 0))
+            return
+        st = np.ascontiguousarray(np.asarray(stored, bool), np.int32)
+        check(lib().mv_set_gene_layout(self._h, st.ctypes.data_as(_i32p), int(st.shape[0])))
 
     def set_mlp_precision(self, dtype: str = "fp32"):
         """Classifier precision of the fitness path: "fp32" (parity default) or "bf16" (perf

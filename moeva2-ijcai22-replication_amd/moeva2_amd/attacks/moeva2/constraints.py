@@ -108,7 +108,7 @@ class TabularConstraints(Constraints):
         self._provision_constraints_min_max(constraints_path)
         self._provision_feature_constraints(feature_path)
         self._fit_scaler()
-        self._engine = None
+        self._engines = {}  # device index -> constraint-only Engine
 
     # -- provisioning (pandas.read_csv exactly like the reference: its C parser decides
     #    the last bits of the bounds)
@@ -171,13 +171,21 @@ class TabularConstraints(Constraints):
         return feature_min, feature_max
 
     # -- device evaluation
-    def _constraint_engine(self):
-        if self._engine is None:
+    def _constraint_engine(self, device=None):
+        """The constraint-only engine on ``device`` (default: torch's current device), built
+        on first use; every device gets its own, so a caller never hands one GPU's buffers
+        to an engine on another."""
+        import torch
+
+        dev = torch.cuda.current_device() if device is None else int(device)
+        eng = self._engines.get(dev)
+        if eng is None:
             from ...problem import build_device_program
             from ..._native import Engine
 
-            self._engine = Engine(build_device_program(self), None, None)
-        return self._engine
+            eng = self._engines[dev] = Engine(build_device_program(self), None, None,
+                                              device=dev)
+        return eng
 
     def evaluate(self, x: np.ndarray, use_tensors: bool = False) -> np.ndarray:
         if use_tensors:
@@ -186,9 +194,9 @@ class TabularConstraints(Constraints):
 
         x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float64)
         eng = self._constraint_engine()
-        xd = torch.from_numpy(x).cuda()
+        xd = torch.from_numpy(x).cuda(eng.device)
         g = torch.empty((x.shape[0], eng.prog.C), dtype=torch.float64, device=xd.device)
-        eng.constraints(xd, g)
+        eng.constraints(xd, g, stream=torch.cuda.current_stream(xd.device))
         return g.cpu().numpy()
 
 

@@ -112,7 +112,27 @@ class Moeva2:
         """RNSGA3: n_ref_points * n_aspiration_dirs (1) + n_obj."""
         return self._n_pop + N_OBJ
 
-    def generate(self, x: np.ndarray, minimize_class, return_device=False, first_state=0):
+    def _engine(self):
+        eng = get_engine(self._constraints, self._get_classifier(), self._ml_scaler, self.norm,
+                         self._scale_objectives, self.device)
+        return eng
+
+    def _bounds(self, x):
+        bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
+        xl = np.array([b[0] for b in bounds], np.float64).reshape(x.shape)
+        xu = np.array([b[1] for b in bounds], np.float64).reshape(x.shape)
+        return xl, xu
+
+    def gene_layout(self, x: np.ndarray) -> np.ndarray:
+        """The engine's gene layout for a job over the states x (bool [V], True = stored;
+        mv_gene_layout).  Pass it to generate(..., gene_layout=) of every batch or shard of
+        the job so each state runs in the same layout whichever states share its batch."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        xl, xu = self._bounds(x)
+        return self._engine().gene_layout(x, xl, xu)
+
+    def generate(self, x: np.ndarray, minimize_class, return_device=False, first_state=0,
+                 gene_layout=None):
         if isinstance(minimize_class, (int, np.integer)):
             minimize_class = np.repeat(minimize_class, x.shape[0])
         minimize_class = np.asarray(minimize_class)
@@ -129,14 +149,13 @@ class Moeva2:
         if B == 0:  # the reference's list comprehension over no states
             return self._empty_device() + (None,) if return_device else []
         clf = self._get_classifier()
-        eng = get_engine(self._constraints, clf, self._ml_scaler, self.norm,
-                         self._scale_objectives, self.device)
+        eng = self._engine()
         eng.set_crossover(self._crossover, self._sbx_eta)
         eng.set_mlp_precision(self._mlp_dtype)
         eng.set_state_streams(self._state_streams, first_state)
-        bounds = [self._constraints.get_feature_min_max(dynamic_input=xi) for xi in x]
-        xl = np.array([b[0] for b in bounds], np.float64)
-        xu = np.array([b[1] for b in bounds], np.float64)
+        xl, xu = self._bounds(x)
+        # engine extension: a job split into batches / shards passes the whole job's layout
+        eng.set_gene_layout(gene_layout)
         eng.set_states(x, xl, xu, minimize_class)
         P, O = self.pop_size(), self._n_offsprings
         seed = self._seed if self._seed is not None else secrets.randbits(63)
@@ -177,9 +196,12 @@ class Moeva2:
         final populations of every state to every rank: genes (B, P, V), F (B, P, 3)."""
         from ...distributed import generate_sharded
 
+        layout = self.gene_layout(x)  # the whole job's: a state's layout is its shard's
+
         def attack(xs, mcs):
             genes, F, _ = self.generate(xs, mcs, return_device=True,
-                                        first_state=_shard_offset(x.shape[0], group))
+                                        first_state=_shard_offset(x.shape[0], group),
+                                        gene_layout=layout)
             return genes, F
 
         return generate_sharded(attack, x, minimize_class, group, empty=self._empty_device)
@@ -200,10 +222,12 @@ class Moeva2:
 
         D = int(x.shape[1])
         dev = torch.device("cuda", self.device)
+        layout = self.gene_layout(x)
 
         def attack(xs, mcs):
             genes, _, _ = self.generate(xs, mcs, return_device=True,
-                                        first_state=_shard_offset(x.shape[0], group))
+                                        first_state=_shard_offset(x.shape[0], group),
+                                        gene_layout=layout)
             xf = torch.empty((genes.shape[0], genes.shape[1], D), dtype=torch.float64,
                              device=dev)
             self.last_engine.decode(genes, xf)

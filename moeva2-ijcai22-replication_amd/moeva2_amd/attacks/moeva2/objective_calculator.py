@@ -27,7 +27,7 @@ from .utils import get_ohe_masks
 class ObjectiveCalculator:
     def __init__(self, classifier: Classifier, constraints: Constraints, minimize_class: int,
                  thresholds: dict, min_max_scaler, norm=np.inf, ml_scaler=None,
-                 problem_class=None, n_jobs=1):
+                 problem_class=None, n_jobs=1, device=None):
         self._classifier = classifier
         self._constraints = constraints
         self._thresholds = thresholds
@@ -38,16 +38,26 @@ class ObjectiveCalculator:
         self._min_max_scaler = min_max_scaler
         self.norm = norm
         self.n_jobs = n_jobs
-        self._dev = None
+        # engine extension: the GPU of the host-array entry points (None: torch's current
+        # device); calculate_objectives_device runs on the device its tensors live on
+        self.device = device
+        self._devs = {}  # device index -> (ObjCalc, constraint engine, Mlp)
 
     # -- device objects (built on first use)
-    def _device(self):
-        """(ObjCalc, constraint engine or None, device classifier or None).  A Constraints
-        object without a device program, or a classifier that is not a Dense MLP, is
-        evaluated through its own ``evaluate`` / ``predict_proba`` on the host (the
+    def _device(self, device=None):
+        """(ObjCalc, constraint engine or None, device classifier or None) on ``device``
+        (default: ``self.device``, else torch's current device), built once per device.  A
+        Constraints object without a device program, or a classifier that is not a Dense MLP,
+        is evaluated through its own ``evaluate`` / ``predict_proba`` on the host (the
         reference accepts any plugin, objective_calculator.py:44-64); the one-hot term, CV
         sum, scaling checks and distance stay on the device (mv_objcalc_score)."""
-        if self._dev is None:
+        import torch
+
+        if device is None:
+            device = self.device if self.device is not None else torch.cuda.current_device()
+        device = int(device)
+        objs = self._devs.get(device)
+        if objs is None:
             from ..._native import Mlp, ObjCalc
             from ...problem import has_device_classifier, has_device_program
 
@@ -59,17 +69,17 @@ class ObjectiveCalculator:
                          np.asarray(self._min_max_scaler.min_, np.float64),
                          None if mls is None else np.asarray(mls.scale_, np.float64),
                          None if mls is None else np.asarray(mls.min_, np.float64),
-                         self.norm)
+                         self.norm, device=device)
             ceng = None
             if (hasattr(self._constraints, "_constraint_engine")
                     and has_device_program(self._constraints)):
-                ceng = self._constraints._constraint_engine()
+                ceng = self._constraints._constraint_engine(device)
             mlp = None
             if has_device_classifier(self._classifier):
                 w = self._classifier.dense_weights()
-                mlp = Mlp(w.weights, w.biases)
-            self._dev = (oc, ceng, mlp)
-        return self._dev
+                mlp = Mlp(w.weights, w.biases, device=device)
+            objs = self._devs[device] = (oc, ceng, mlp)
+        return objs
 
     def calculate_objectives_3d(self, x_initials, x):
         """Batched ``_calculate_objective``: x_initials (B, D), x (B, n, D) -> (B, n, 3).
@@ -89,18 +99,19 @@ class ObjectiveCalculator:
             return np.zeros((B, n, 3))
         oc, ceng, mlp = self._device()
         dev = torch.device("cuda", oc.device)
+        st = torch.cuda.current_stream(dev)
         xi = torch.from_numpy(x_initials).to(dev)
         xd = torch.from_numpy(x).to(dev)
         obj = torch.empty((B, n, 3), dtype=torch.float64, device=dev)
         bad = torch.empty((B, n), dtype=torch.int32, device=dev)
         if ceng is not None and mlp is not None:
-            oc.run(ceng, mlp, xi, xd, self._minimize_class, obj, bad)
+            oc.run(ceng, mlp, xi, xd, self._minimize_class, obj, bad, stream=st)
         else:
             x_f = x.reshape(B * n, D)
             if ceng is not None:
                 G = torch.empty((B * n, ceng.prog.C), dtype=torch.float64, device=dev)
                 if ceng.prog.C > 0:
-                    ceng.constraints(xd.view(B * n, D), G)
+                    ceng.constraints(xd.view(B * n, D), G, stream=st)
             else:  # objective_calculator.py:50: the plugin's own numpy evaluate
                 g = np.ascontiguousarray(self._constraints.evaluate(x_f), np.float64)
                 G = torch.from_numpy(g.reshape(B * n, -1)).to(dev)
@@ -108,12 +119,12 @@ class ObjectiveCalculator:
             if mlp is not None:
                 xm = torch.from_numpy(np.ascontiguousarray(x_ml, np.float64)).to(dev)
                 proba = torch.empty((B * n, mlp.n_out), dtype=torch.float64, device=dev)
-                mlp.predict(xm, proba)
+                mlp.predict(xm, proba, stream=st)
             else:  # :64 Classifier.predict_proba of any model
                 p = np.ascontiguousarray(self._classifier.predict_proba(x_ml), np.float64)
                 proba = torch.from_numpy(p.reshape(B * n, -1)).to(dev)
             oc.score(xi, xd, G if G.shape[1] > 0 else None, proba, self._minimize_class, obj,
-                     bad)
+                     bad, stream=st)
         # objective_calculator.py:72-76: the scaled origin and candidates must lie in [0, 1]
         assert not bool(bad.any().item()), "candidate or initial state outside the scaler range"
         return obj.cpu().numpy()
@@ -124,7 +135,10 @@ class ObjectiveCalculator:
         device constraint program and classifier (host plugins: calculate_objectives_3d)."""
         import torch
 
-        oc, ceng, mlp = self._device()
+        if not (x.is_cuda and x_initials.is_cuda) or x.device != x_initials.device:
+            raise ValueError(f"x ({x.device}) and x_initials ({x_initials.device}) must be "
+                             "tensors on one GPU")
+        oc, ceng, mlp = self._device(x.device.index)
         if ceng is None or mlp is None:
             raise ValueError("calculate_objectives_device needs the device constraint program "
                              "and classifier; use calculate_objectives_3d for host plugins")
@@ -133,7 +147,8 @@ class ObjectiveCalculator:
         if B * n == 0:
             return obj
         bad = torch.empty((B, n), dtype=torch.int32, device=x.device)
-        oc.run(ceng, mlp, x_initials.contiguous(), x.contiguous(), self._minimize_class, obj, bad)
+        oc.run(ceng, mlp, x_initials.contiguous(), x.contiguous(), self._minimize_class, obj, bad,
+               stream=torch.cuda.current_stream(x.device))
         assert not bool(bad.any().item()), "candidate or initial state outside the scaler range"
         return obj
 

@@ -82,9 +82,14 @@ def success_flags(obj, x_f, thresholds):
     x_f (b, n, D): the candidates in ML space.  Returns
       flags (b, 7) uint8: o1..o7 of _objective_respected (:86-101) reached by at least one
         candidate of the state (success_rate_3d's per-state "> 0", :121-128);
-      best (b, D) float64: the o7-successful candidate with the smallest f1 -- what
-        _get_one_successful(preferred_metrics="misclassification", max_inputs=1) keeps
-        (:153-182; equal f1: the lowest index) -- NaN where the state has none.
+      best (b, D) float64: the candidate _get_one_successful(preferred_metrics=
+        "misclassification", max_inputs=1) returns (:153-182) -- NaN where the state has no
+        o7-successful candidate.  The reference indexes the f1 argsort with the o7 mask in
+        ORIGINAL row order (``sorted_index[objective_respected[:, -1]][:1]``), i.e. it keeps
+        sorted_index[k0] for the first o7-successful row k0: the candidate with the
+        (k0+1)-th smallest f1, which need not be successful itself.  That is reproduced
+        here, with a stable f1 sort (numpy's default argsort orders equal f1 in an
+        implementation-defined way).
     NaN objectives compare false, as in numpy."""
     import torch
 
@@ -99,8 +104,9 @@ def success_flags(obj, x_f, thresholds):
     D = x_f.shape[-1]
     best = torch.full((b, D), float("nan"), dtype=torch.float64, device=x_f.device)
     if b and n:
-        key = torch.where(resp[..., 6], f1, torch.full_like(f1, float("inf")))
-        idx = torch.argmin(key, dim=1)  # first minimal index
+        order = torch.sort(f1, dim=1, stable=True).indices  # np.argsort(f1) (NaN last)
+        k0 = torch.argmax(resp[..., 6].to(torch.uint8), dim=1)  # first o7-successful row
+        idx = order[torch.arange(b, device=obj.device), k0]
         ok = flags[:, 6] != 0
         rows = x_f[torch.arange(b, device=x_f.device), idx]
         best[ok] = rows[ok].to(torch.float64)

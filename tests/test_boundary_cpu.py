@@ -186,3 +186,26 @@ def test_safe_loaders_execute_nothing():
         assert isinstance(rec, Obj) and rec.cls == "os.system" and rec.args == ("true",)
     finally:
         os.remove(p)
+
+
+def test_objective_calculator_device_path_refuses_host_or_mixed_tensors():
+    """calculate_objectives_device runs on the GPU its tensors live on and builds its device
+    objects there; host tensors (or tensors of two devices) are refused before any engine
+    call (the objects used to be built on device 0 whatever the tensors' GPU)."""
+    import torch
+
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+
+    class _Cons:
+        def get_feature_type(self):
+            return np.array(["real"] * 4)
+
+        def get_mutable_mask(self):
+            return np.ones(4, bool)
+
+    calc = ObjectiveCalculator.__new__(ObjectiveCalculator)
+    calc._devs = {}
+    with pytest.raises(ValueError, match="one GPU"):
+        calc.calculate_objectives_device(torch.zeros(2, 4, dtype=torch.float64),
+                                         torch.zeros(2, 3, 4, dtype=torch.float64))
+    assert calc._devs == {}

@@ -160,15 +160,21 @@ def fake_scored_objectives(x):
 def ref_success(obj, xf):
     """numpy restatement of objective_calculator.py:86-101 (_objective_respected), :121-128
     (any over the population) and :153-182 (_get_one_successful, misclassification asc,
-    max_inputs=1; stable order among equal f1)."""
-    flags, best = [], []
+    max_inputs=1), literally: the f1 argsort indexed by the o7 mask in original row order
+    (stable order among equal f1).  Also returns how many states the plain "o7-successful
+    row of smallest f1" rule would answer differently."""
+    flags, best, differs = [], [], 0
     for o, x in zip(obj, xf):
         c, m, l = o[:, 0] <= 0, o[:, 1] < THR["f1"], o[:, 2] <= THR["f2"]
         r = np.column_stack([c, m, l, c * m, c * l, m * l, c * m * l])
         flags.append(r.any(axis=0))
-        idx = np.argsort(o[:, 1], kind="stable")[r[:, -1][np.argsort(o[:, 1], kind="stable")]]
-        best.append(x[idx[0]] if idx.size else np.full(x.shape[1], np.nan))
-    return np.array(flags), np.array(best)
+        sorted_index = np.argsort(o[:, 1], kind="stable")
+        sel = sorted_index[r[:, -1]][:1]
+        best.append(x[sel[0]] if sel.size else np.full(x.shape[1], np.nan))
+        if sel.size:
+            naive = int(np.argmin(np.where(r[:, -1], o[:, 1], np.inf)))
+            differs += int(not np.array_equal(x[naive], x[sel[0]]))
+    return np.array(flags), np.array(best), differs
 
 
 def _scored_worker(rank, world, port, B, q):
@@ -214,8 +220,9 @@ def test_scored_sharded_gathers_flags(B, world):
         assert pr.exitcode == 0
     x = np.arange(B * 5, dtype=np.float64).reshape(B, 5)
     obj, xf = fake_scored_objectives(x)
-    ref_f, ref_b = ref_success(obj.numpy(), xf.numpy())
+    ref_f, ref_b, differs = ref_success(obj.numpy(), xf.numpy())
     assert ref_f[:, 6].any() and not ref_f[:, 6].all() or B < 3
+    assert differs > 0 or B < 5  # the reference's indexing is what is checked
     per = -(-B // world)
     for rank, calls, flags, best in res:
         assert flags.dtype == np.uint8 and flags.shape == (B, 7)

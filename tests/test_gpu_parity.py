@@ -737,6 +737,66 @@ def test_compact_layout_tracks_full_layout(monkeypatch, cx):
     np.testing.assert_array_equal(F1n[..., 2], F2n[..., 2])
 
 
+def test_gene_layout_is_the_jobs_not_the_batchs():
+    """The compact layout is derived from the states it is bound with.  A job split into
+    batches or shards (generate_sharded) passes the WHOLE job's layout (mv_gene_layout ->
+    mv_set_gene_layout), so a state runs in the same layout whichever states share its batch.
+    Here state 4 has a non-integral value in one of the 120 fixed features: the job keeps that
+    gene stored, a batch of states 0-2 alone would not, and with the job's layout the batch's
+    results are bit-identical to the job's.  A layout that leaves out a gene some bound state
+    can change is refused."""
+    from moeva2_amd._native import NativeError
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+
+    name = "botnet"
+    c = make_constraints(name)
+    p = Project(name)
+    m = Moeva2(os.path.join(RES, PROJECTS[name][1]), c, ml_scaler=make_scaler(name), norm=2,
+               n_gen=5, n_pop=40, n_offsprings=20, seed=7, state_streams=True)
+    X = p.x[:6].copy()
+    lay0 = m.gene_layout(X)
+    assert (~lay0).sum() == 120
+    g = int(np.where(~lay0)[0][0])
+    f = int(np.where(p.lay.mutable_mask)[0][g])  # IDENT: gene g <-> mutable feature g
+    X[4, f] += 0.5
+    lay = m.gene_layout(X)
+    assert lay[g] and (~lay).sum() == 119
+    assert (~m.gene_layout(X[:3])).sum() == 120  # the batch alone would leave gene g out
+    g_job, F_job, _ = m.generate(X, 1, return_device=True)
+    assert np.array_equal(m.last_engine.stored_genes(), lay)
+    g_b, F_b, _ = m.generate(X[:3], 1, return_device=True, gene_layout=lay)
+    assert np.array_equal(m.last_engine.stored_genes(), lay)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(g_b.cpu().numpy(), g_job.cpu().numpy()[:3])
+    np.testing.assert_array_equal(F_b.cpu().numpy(), F_job.cpu().numpy()[:3])
+    m.generate(X[:3], 1, return_device=True)  # default: the batch's own layout again
+    assert (~m.last_engine.stored_genes()).sum() == 120
+    with pytest.raises(NativeError, match="not fixed"):
+        m.generate(X, 1, return_device=True, gene_layout=lay0)
+
+
+def test_device_buffers_of_another_gpu_are_refused():
+    """Entry points check that their buffers live on the engine's GPU (api.cpp on_device):
+    a one-GPU box can only show that buffers of the engine's own device pass and that the
+    ObjectiveCalculator builds its objects on the device of its tensors."""
+    from moeva2_amd.attacks.moeva2.objective_calculator import ObjectiveCalculator
+
+    name = "botnet"
+    c, sc = make_constraints(name), make_scaler(name)
+    calc = ObjectiveCalculator(make_classifier(name), c, 1, {"f1": 0.5, "f2": 4.0},
+                               min_max_scaler=sc, ml_scaler=sc, norm=2)
+    p = Project(name)
+    xi = torch.from_numpy(p.x[:2]).cuda()
+    x = xi[:, None, :].repeat(1, 3, 1).contiguous()
+    obj = calc.calculate_objectives_device(xi, x)
+    assert list(calc._devs) == [0] and calc._devs[0][0].device == 0
+    assert calc._devs[0][1].device == 0 and calc._devs[0][2].device == 0
+    np.testing.assert_array_equal(obj.cpu().numpy(), calc.calculate_objectives_3d(p.x[:2],
+                                                                                   x.cpu().numpy()))
+    with pytest.raises(ValueError):
+        calc.calculate_objectives_device(xi.cpu(), x)
+
+
 def test_attack_invariants_lcld():
     """Whole device loop: bounds, integrality, F == re-evaluation, history layout.  (Each
     generation's kernels are pinned bit-exactly above; the loop is compared end to end
@@ -844,7 +904,7 @@ def test_generate_scored_sharded_real_engine_world1():
     """Moeva2.generate_scored_sharded on a one-rank RCCL group: the gathered per-state o1..o7
     flags equal the ObjectiveCalculator's verdict on an unsharded generate of the same states
     (success_rate_3d, objective_calculator.py:121-128), the successful candidates are the
-    o7-successful rows with the smallest f1 (_get_one_successful, :153-182), and per-state
+    reference's _get_one_successful(max_inputs=1) picks (:153-182), and per-state
     streams keyed by the global state index give the same populations unsharded."""
     import socket
 
@@ -882,8 +942,13 @@ def test_generate_scored_sharded_real_engine_world1():
     for b in range(X.shape[0]):
         ok = resp[b][:, 6]
         if ok.any():
-            f1 = np.where(ok, obj[b][:, 1], np.inf)
-            np.testing.assert_array_equal(best[b], x_f[b][int(np.argmin(f1))])
+            # _get_one_successful(max_inputs=1) literally: the f1 argsort indexed by the o7
+            # mask in original row order (stable among equal f1)
+            sorted_index = np.argsort(obj[b][:, 1], kind="stable")
+            np.testing.assert_array_equal(best[b], x_f[b][sorted_index[ok][0]])
+            sel = calc._select_successful(obj[b], x_f[b], "misclassification", "asc", 1)
+            assert np.sort(obj[b][:, 1])[np.argmax(ok)] == obj[b][sorted_index[ok][0], 1]
+            assert sel.shape == (1, x_f.shape[2])
         else:
             assert np.isnan(best[b]).all()
 
