@@ -1276,8 +1276,14 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
       afast += (double)(q[10] - q[5]);
       nflag += (double)q[12];
     }
-    std::fprintf(stderr, " | ideal/worst=%.0f assoc_fast=%.0f flagged=%.1f", red / e->B,
-                 afast / e->B, nflag / e->B);
+    double tplan = 0.0, ttour = 0.0;
+    for (int b = 0; b < e->B; ++b) {
+      const long long* q = &ph[(size_t)b * 32];
+      tplan += (double)(q[24] - q[23]);
+    }
+    std::fprintf(stderr, " | ideal/worst=%.0f assoc_fast=%.0f flagged=%.1f plan=%.0f", red / e->B,
+                 afast / e->B, nflag / e->B, tplan / e->B);
+    (void)ttour;
     // the launch lasts as long as its slowest state: per-phase maxima and the total's tail
     std::vector<double> tot(e->B);
     double pmax[10] = {0};

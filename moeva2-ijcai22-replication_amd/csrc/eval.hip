@@ -241,6 +241,7 @@ template <bool IDENT, int NT, bool SBX, bool PLAN = false, bool EARLY = false>
 __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
                                         unsigned char* smem) {
   static_assert(!EARLY || (IDENT && PLAN && !SBX), "early staging: k_genc two-point only");
+  constexpr bool FUSED = EARLY && MV_GENC_FUSED;  // the constraints inside the row loop
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -249,7 +250,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const int V = p.V, Dm = p.Dm, Dm4 = p.Dm4;
   const bool ev = a.do_eval != 0;
   const VaryOff o = vary_offsets(p);
-  const GenLds L = EARLY ? genc_early_lds(o, p) : gen_lds(o, REGC, IDENT, ev);
+  const GenLds L = FUSED ? genc_fused_lds(o, p) : EARLY ? genc_early_lds(o, p)
+                                                      : gen_lds(o, REGC, IDENT, ev);
   const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
   // the rows' matings and destinations first: their round trips (the parents come from the
   // previous k_survive) overlap the LDS staging instead of following it
@@ -281,6 +283,19 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       }
     }
     orow_v = MV_IDX(a.out_map ? a.out_map[(size_t)b * a.n + irow] : irow, a.out_rows, CK_GEN_DST);
+  }
+  // FUSED: the constraint program's packed lane-op words, straight from the problem blob
+  const int n_lane_ops = p.C - p.n_sumdiff;
+  const int kops = min(OPS_REG, (n_lane_ops + 63) >> 6);
+  unsigned opw[OPS_REG];
+  if (FUSED) {
+    const unsigned* gw = (const unsigned*)(p.vblob + o.s_opw);
+#pragma unroll
+    for (int k = 0; k < OPS_REG; ++k) {
+      const int c = lane + 64 * k;
+      const unsigned w_ = gw[c < n_lane_ops ? c : 0];
+      opw[k] = (k < kops && c < n_lane_ops) ? w_ : 0u;
+    }
   }
   if (EARLY) {  // phase 2's program + x_init, phase 1's encoder (and scaler) coefficients
     const unsigned ssz = o.s_end - o.s_at;
@@ -339,6 +354,25 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const double* s_em = (const double*)(smem + L.e_at + (o.em - o.e_at));
   const double* s_x0 = (const double*)(smem + L.e_at + (o.x0 - o.e_at));
   double* xrow = (double*)(smem + L.rows_at + wave * o.rb);
+  // FUSED: the wave's slim row buffer (stored mutable features, SlotRow) and the program's
+  // LDS tables (region S at 0, x_init at L.x_at)
+  double* frow = (double*)(smem + L.rows_at + wave * o.rbs);
+  OpTab ftab;
+  ftab.code = nullptr;
+  ftab.arg = nullptr;
+  ftab.k = nullptr;
+  ftab.k1 = (const double*)(smem + (o.s_k - o.s_at));
+  ftab.sd = (const int4*)(smem + (o.s_sd - o.s_at));
+  ftab.col = (const int*)(smem + (o.s_col - o.s_at));
+  ftab.pool = (const int*)(smem + (o.s_pool - o.s_at));
+  ftab.C = p.C;
+  ftab.n_lane = n_lane_ops;
+  ftab.tol = p.tol;
+  if (a.hist) {
+    ftab.hlo = a.hist + (size_t)b * a.hist_rows * a.hist_w;
+    ftab.hhi = ftab.hlo + (size_t)a.hist_rows * a.hist_w;
+  }
+  const SlotRow fsrow{frow, (const double*)(smem + L.x_at), p.Dm};
   if (ev && !IDENT) {  // immutable features of this wave's row buffer (written once)
     const double* s_xi = (const double*)(smem + L.x_at);
     for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
@@ -437,17 +471,38 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       }
       wave_sync();  // the next row's scatter overwrites xrow
     }
+    if constexpr (FUSED) {  // the child into the wave's row buffer for the program below
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (lane + 64 * t < Vo) frow[lane + 64 * t] = x[t];
+    }
     acc = l2 ? wave_sum(acc) : wave_max(acc);
+    double f3 = 0.0;
+    double* hrow = nullptr;
+    if constexpr (FUSED) {  // k_cons's do_row on the registers' child (cons_rows, SLIM)
+      wave_sync();
+      hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows +
+                                MV_IDX(hist_row0 + i, a.hist_rows, CK_CONS_DST)) * a.hist_w
+                    : nullptr;
+      double* hc = (hrow && a.hist_w > 3) ? hrow + 3 : nullptr;
+      double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
+      f3 = constraints_regs<false, true>(ftab, opw, kops, fsrow, lane, grow, hc);
+    }
     if (lane == 0) {
       double f2 = l2 ? sqrt(acc) : acc;
       if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;
-      if (a.F)
-        a.F[(size_t)b * a.out_rows * 3 + MV_IDX((size_t)orow * 3 + 1, a.out_rows * 3, CK_AT_F2)] = f2;
+      if (a.F) {
+        double* Fr = a.F + (size_t)b * a.out_rows * 3;
+        Fr[MV_IDX((size_t)orow * 3 + 1, a.out_rows * 3, CK_AT_F2)] = f2;
+        if (FUSED) Fr[MV_IDX((size_t)orow * 3 + 2, a.out_rows * 3, CK_AT_F3)] = f3;
+      }
       if (a.hist)
         a.hist[(size_t)b * a.hist_rows * a.hist_w +
                MV_IDX((size_t)MV_IDX(hist_row0 + i, a.hist_rows, CK_GEN_ROW) * a.hist_w + 1,
                       (long long)a.hist_rows * a.hist_w, CK_AT_HIST1)] = f2;
+      if (FUSED && hrow) *MV_PTR(hrow + 2, ftab.hlo, ftab.hhi, CK_AT_HIST2) = f3;
     }
+    if constexpr (FUSED) wave_sync();  // the next row overwrites the row buffer
   };
   for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
     double x[NT];
@@ -736,9 +791,11 @@ __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows
   // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
   // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them.  Both
   // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  cons_rows<false, IDENT, NT, SLIM, EARLY>(a, hist_row0, rows_wg, smem, true, orow_v);
+  if (!(EARLY && MV_GENC_FUSED)) {  // FUSED: the constraints ran inside phase 1's row loop
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    cons_rows<false, IDENT, NT, SLIM, EARLY>(a, hist_row0, rows_wg, smem, true, orow_v);
+  }
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 7] = wall_clock64();
@@ -1998,7 +2055,10 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const bool slim = a.p.slim != 0;
     const size_t lc = slim ? cons_lds_slim(o) : cons_lds_total(o);
     static const size_t pad = lds_pad("MV_LDS_PAD_GENC");
-    const size_t lds = (slim && !sbx ? genc_early_lds(o, a.p).total : (lg > lc ? lg : lc)) + pad;
+    const size_t lds = (slim && !sbx ? (MV_GENC_FUSED ? genc_fused_lds(o, a.p).total
+                                                      : genc_early_lds(o, a.p).total)
+                                     : (lg > lc ? lg : lc)) +
+                       pad;
     // k_genc takes mode 1's draws from the variation plan (mv_attack_run's k_survive)
     if (a.mode == 1 && !(a.plan_hdr && a.plan_mw && a.plan_mu)) return hipErrorInvalidValue;
     if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);

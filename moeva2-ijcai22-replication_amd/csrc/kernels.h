@@ -149,6 +149,24 @@ __host__ __device__ inline GenLds genc_early_lds(const VaryOff& o, const DProble
   l.total = rows_at + (ph1 > ph2 ? ph1 : ph2);
   return l;
 }
+// MV_GENC_FUSED (k_genc's two-point slim instance): the constraint program runs inside
+// phase 1's row loop on the child genes still in registers -- no second row loop, no
+// re-read of the children, no phase barrier.  LDS: [S][X][E (and C)][one row per wave].
+#ifndef MV_GENC_FUSED
+#define MV_GENC_FUSED 1
+#endif
+__host__ __device__ inline GenLds genc_fused_lds(const VaryOff& o, const DProblem& p) {
+  GenLds l{};
+  const unsigned ssz = o.s_end - o.s_at;
+  const unsigned e_sz = o.sb - o.e_at;
+  l.b_at = 0;
+  l.x_at = ssz;
+  l.e_at = ssz + o.x_end;
+  l.c_at = l.e_at + e_sz;
+  l.rows_at = l.c_at + (p.xml_direct ? 0u : (o.c_end - o.c_at));
+  l.total = l.rows_at + CONS_W * o.rbs;
+  return l;
+}
 // SBX rows: a per-wave list of the crossed genes (int) and their children (double) after the
 // k_gen layout (rowops.h sbx_row)
 __host__ __device__ inline unsigned gen_sbx_at(const GenLds& l) { return (l.total + 15u) & ~15u; }

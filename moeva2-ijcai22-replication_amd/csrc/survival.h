@@ -32,7 +32,16 @@ static __device__ double g_surv_dump[SURV_DUMP_N];
 
 namespace mv {
 
-constexpr int SURV_TMAX = 1024;  // largest survival workgroup (reduction scratch sizing)
+constexpr int SURV_TMAX = 1024;
+// MV_ASSOC_F64: the association pre-filter in fp64 (directions as double4 in LDS) instead of
+// fp32 with crowded-direction refinement
+#ifndef MV_ASSOC_F64
+#define MV_ASSOC_F64 1
+#endif
+// its first sweep's unroll (2: 104 VGPRs, two survival workgroups per CU; 1: 80, three)
+#ifndef MV_ASSOC_UNROLL
+#define MV_ASSOC_UNROLL 1
+#endif  // largest survival workgroup (reduction scratch sizing)
 
 struct SurvLds {
   double* F;        // [N*3]
@@ -130,7 +139,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(F, (size_t)NW * 64 * 3 * 8)  // rows past N hold NaN (dominance padding)
   o.ref = 0;                        // unused: a.ref in global memory
   TAKE(U, (size_t)RN * 3 * 8)
-  TAKE(Uf, (size_t)RN * 16)
+  TAKE(Uf, (size_t)RN * (MV_ASSOC_F64 ? 32 : 16))
   TAKE(dist, (size_t)N * 8)
   TAKE(red, (SURV_T / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
@@ -172,6 +181,9 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(dmin, (size_t)RN * 8)
   TAKE(lround, (size_t)(2 * N + 2) * 4)
   unsigned total = alias ? end : off;
+  // N > SURV_NLDS: the rank dominance's words and sort indices (5 RANK_N2 u32) in the
+  // niching temporaries (appended there: the bitsets live in HBM)
+  if (!dom_lds && total < o.count + 5u * 1024u * 4u) total = o.count + 5u * 1024u * 4u;
   if (ptab_words > 0 && (size_t)ptab_words * 4 > (size_t)NW * 64 * 3 * 8) {
     off = total;
     TAKE(ptab, (size_t)ptab_words * 4)
@@ -343,50 +355,232 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
   }
 }
 
-// The next generation's variation plan (engine.h VPlan) of state b: thread i < O_next takes
-// offspring row i -- its parents from the tournament (par: LDS, 2 per mating), the two
-// crossover subsets' draws (rowops cx_sub, as row_draws), and its mutations: the same
-// geometric-gap walk over the Vr genes as the row kernels (Philox index i * MUT_J + j,
-// TAG_MUT_MASK), positions mapped to stored genes (a fixed gene's draw is consumed, nothing
-// is written), at most PLAN_MUT kept (more: the overflow flag).  geo / cmap / ginfo: LDS.
+// The next generation's variation plan (engine.h VPlan) of state b, with every thread: (1)
+// the matings' crossover draws (cx_sub, item 2 m + subset) into LDS cxs; (2) the mutations:
+// four lanes per offspring row i (lanes 4 k + q of a wave; T is a multiple of 64, so a group
+// never straddles waves), lane q taking draw q of the row's geometric-gap walk over the Vr
+// genes (Philox index i * MUT_J + q, TAG_MUT_MASK) -- the same draws and positions as walking
+// them one after another (prefix sums of the 1 + gap steps inside the group), in one round;
+// a position maps to its stored gene (a fixed gene's draw is consumed, nothing is written)
+// and the row's stored hits take the plan's slots in draw order.  A row whose fourth
+// position is still inside the genes is finished by its lane 3, serially (2 % of the rows);
+// more than PLAN_MUT stored mutations set the overflow flag.  par: the tournament's parents
+// (LDS, 2 per mating); geo / cmap / ginfo: LDS.
 template <int T>
 __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, const int gen,
-                                               const int* par, const uint32_t* geo,
+                                               const int* par, int* cxs, const uint32_t* geo,
                                                const int* cmap, const int* ginfo) {
+  static_assert(T % 64 == 0, "variation_plan: groups of four lanes inside a wave");
   const int n = a.O_next, nm = n / 2;
+  const int tid = threadIdx.x, lane = tid & 63;
   const Rng rng(a.seed, state_stream(a.stream_key, a.state_keys, a.key0, b));
+  for (int t = tid; t < 2 * nm; t += T) {
+    int c = pack_cx(cx_sub(rng, gen, t >> 1, t & 1, (t & 1) ? a.n_sub1 : a.n_sub0, a.cx_prob));
+    if (a.cx_sbx) c &= 1;
+    cxs[t] = c;
+  }
+  __syncthreads();
   const int Vr = a.Vr;
   const float lq = __log2f(1.0f - 1.0f / (float)Vr);
-  for (int i = threadIdx.x; i < n; i += T) {
+  for (int t0 = 0; t0 < 4 * n; t0 += T) {  // uniform trip count
+    const int t = t0 + tid;
+    const bool live = t < 4 * n;
+    const int i = live ? t >> 2 : 0, q = t & 3;
     const int m = i % nm, side = i / nm;
-    const int p0 = par[2 * m], p1 = par[2 * m + 1];
-    const int pv = side ? (p1 | (p0 << 16)) : (p0 | (p1 << 16));
-    int c0 = pack_cx(cx_sub(rng, gen, m, 0, a.n_sub0, a.cx_prob));
-    int c1 = pack_cx(cx_sub(rng, gen, m, 1, a.n_sub1, a.cx_prob));
-    if (a.cx_sbx) {
-      c0 &= 1;
-      c1 &= 1;
+    int st = 0;
+    double uq = 0.0;
+    if (live) {
+      const u32x4 w = rng.draw((uint32_t)(i * MUT_J + q), (uint32_t)gen, TAG_MUT_MASK);
+      st = 1 + geo_gap(geo, Vr, w.x, lq);
+      uq = u53(w.y, w.z);
     }
+    {
+      const int t1 = __shfl(st, (lane + 63) & 63);
+      st += q >= 1 ? t1 : 0;
+      const int t2 = __shfl(st, (lane + 62) & 63);
+      st += q >= 2 ? t2 : 0;
+    }
+    const int pos = st - 1;  // position of draw q (increasing in q)
+    const bool hit = live && pos < Vr;
+    const int cq = hit ? cmap[pos] : -1;
+    const bool stored = cq >= 0;
+    const unsigned long long sm = __ballot(stored);
+    const unsigned grp = (unsigned)((sm >> (lane & ~3)) & 0xFull);
+    const int slot = __popc(grp & ((1u << q) - 1u));  // stored hits before this lane's
+    const int c0 = cxs[2 * m], c1 = cxs[2 * m + 1];
     int* mw = a.plan_mw + ((size_t)b * n + i) * PLAN_MUT;
     double* mu = a.plan_mu + ((size_t)b * n + i) * PLAN_MUT;
-    int cnt = 0, ovf = 0, pos = -1;
-    for (int j = 0;; ++j) {
-      const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
-      pos += 1 + geo_gap(geo, Vr, w.x, lq);
-      if (pos >= Vr) break;
-      const int cq = cmap[pos];
-      if (cq < 0) continue;  // a fixed gene of the compact layout: its mutation is the identity
-      if (cnt == PLAN_MUT) {
-        ovf = 1;
-        break;
-      }
-      const int gi = ginfo[MV_IDX(cq, a.V, CK_GEN_MUTPOS)];
+    auto put = [&](int k, int g, double u) {
+      const int gi = ginfo[MV_IDX(g, a.V, CK_GEN_MUTPOS)];
       const int oth = (!a.cx_sbx && swapped_packed(gi, c0, c1)) ? 1 : 0;
-      mw[cnt] = cq | (((gi & 3) == 0 ? 1 : 0) << 16) | (oth << 17);
-      mu[cnt] = u53(w.y, w.z);
-      ++cnt;
+      mw[k] = g | (((gi & 3) == 0 ? 1 : 0) << 16) | (oth << 17);
+      mu[k] = u;
+    };
+    if (stored) put(slot, cq, uq);
+    if (live && q == 3) {  // the row's count (and the rare rest of its walk), then its header
+      int cnt = __popc(grp), ovf = 0;
+      if (hit) {
+        int p = pos;
+        for (int j = 4;; ++j) {
+          const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
+          p += 1 + geo_gap(geo, Vr, w.x, lq);
+          if (p >= Vr) break;
+          const int g = cmap[p];
+          if (g < 0) continue;
+          if (cnt == PLAN_MUT) {
+            ovf = 1;
+            break;
+          }
+          put(cnt, g, u53(w.y, w.z));
+          ++cnt;
+        }
+      }
+      const int p0 = par[2 * m], p1 = par[2 * m + 1];
+      const int pv = side ? (p1 | (p0 << 16)) : (p0 | (p1 << 16));
+      a.plan_hdr[(size_t)b * n + i] = make_int4(pv, c0, c1, cnt | (ovf << 4));
     }
-    a.plan_hdr[(size_t)b * n + i] = make_int4(pv, c0, c1, cnt | (ovf << 4));
+  }
+}
+
+// ---- N > SURV_NLDS: dominance from per-objective ranks (MV_DOM_RANKS, default on).
+// r_k(i) = #{j : F_k(j) < F_k(i)} preserves every <, = and > between the values of
+// objective k when none is NaN, so i dominates j (every F_k(i) <= F_k(j), one <) exactly
+// when every r_k(i) <= r_k(j) and the rank triples differ.  The ranks come from three
+// bitonic sorts of the individuals' indices (by value, then index; all three objectives in
+// every stage) and a max-scan of the sorted runs' starts -- O(N log^2 N) instead of the
+// O(N^2) counting of round 4 (whose cost matched the pair pass it replaced).  The pair pass
+// then tests two 16-bit fields with guards in one u32 (P01 = r0 | r1 << 16, guards at bits
+// 15 and 31: (P01j | G) - P01i keeps guard k iff r_k(j) >= r_k(i)) plus one u32 compare for
+// r2 -- 32-bit integer operations instead of six fp64 compares per pair.
+#ifndef MV_DOM_RANKS
+#define MV_DOM_RANKS 1
+#endif
+constexpr int RANK_N2 = 1024;  // padded sort length (N <= SURV_NMAX)
+
+// Sorted index arrays idx[k * RANK_N2 + p] of objective k (ascending value, ties by index,
+// the padding indices >= N last), then ranks into P01 / P2 (u32 words).  All threads; ends
+// on a barrier.  wsum: one int per wave.
+template <int T>
+__device__ __forceinline__ void rank_words(const double* F, const int N, int* idx,
+                                           unsigned* P01, unsigned* P2, int* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int n2 = RANK_N2, h = RANK_N2 / 2;
+  for (int t = tid; t < 3 * n2; t += T) idx[t] = t & (n2 - 1);
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < 3 * h; t += T) {
+        const int k = t / h, tt = t - k * h;
+        const int i = 2 * tt - (tt & (stride - 1));
+        const int j = i + stride;
+        int* ik = idx + k * n2;
+        const int x = ik[i], y = ik[j];
+        bool gt;  // (value, index) of x > that of y; padding indices sort last
+        if (x >= N || y >= N) {
+          gt = (x >= N && y >= N) ? x > y : x >= N;
+        } else {
+          const double vx = F[x * 3 + k], vy = F[y * 3 + k];
+          gt = vx > vy || (vx == vy && x > y);
+        }
+        if (gt == ((i & size) == 0)) {
+          ik[i] = y;
+          ik[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+  // rank of the individual at sorted position q = the start of its run of equal values:
+  // an inclusive max-scan of (q if the value differs from position q - 1, else 0)
+  constexpr int PER = n2 / T;  // positions per thread and objective (contiguous)
+  int rk[3][PER];
+  for (int k = 0; k < 3; ++k) {
+    const int* ik = idx + k * n2;
+    int run = 0;
+    for (int e = 0; e < PER; ++e) {
+      const int q = tid * PER + e;
+      int st = 0;
+      if (q < N) {
+        const int x = ik[q];
+        st = (q == 0 || F[ik[q - 1] * 3 + k] != F[x * 3 + k]) ? q : 0;
+      }
+      run = st > run ? st : run;
+      rk[k][e] = run;
+    }
+    // exclusive max over the threads before this one: wave scan, then the waves' totals
+    int incl = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl = y > incl ? y : incl;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = __shfl_up(incl, 1, 64);
+    if (lane == 0) before = 0;
+    for (int w = 0; w < wave; ++w) before = wsum[w] > before ? wsum[w] : before;
+    for (int e = 0; e < PER; ++e) rk[k][e] = rk[k][e] > before ? rk[k][e] : before;
+    __syncthreads();  // wsum is reused by the next objective
+  }
+  for (int e = 0; e < PER; ++e) {
+    const int q = tid * PER + e;
+    if (q < N) {
+      P01[idx[q]] = 0u;  // fields below are ORed in by objective
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < 3; ++k)
+    for (int e = 0; e < PER; ++e) {
+      const int q = tid * PER + e;
+      if (q < N) {
+        const int x = idx[k * n2 + q];
+        if (k == 0) atomicOr(&P01[x], (unsigned)rk[0][e]);
+        if (k == 1) atomicOr(&P01[x], (unsigned)rk[1][e] << 16);
+        if (k == 2) P2[x] = (unsigned)rk[2][e];
+      }
+    }
+  __syncthreads();
+}
+
+// The dominance work items of the six-compare pass on the rank words: the same bits.
+__device__ __forceinline__ void dominance_items_ranks(SurvLds& L, const int N, const int NW,
+                                                      const int lane, const unsigned* P01,
+                                                      const unsigned* P2) {
+  unsigned short* dom16 = (unsigned short*)L.dom;
+  constexpr unsigned G = 0x80008000u;
+  const int n_q = NW * (NW + 1) * 2;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
+    t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+    if (t >= n_q) break;
+    const int qq = t & 3;
+    int qi = 0, rem = t >> 2;
+    while (rem >= NW - qi) {
+      rem -= NW - qi;
+      ++qi;
+    }
+    const int qj = qi + rem;
+    const int i = qi * 64 + lane;
+    const bool vi = i < N;
+    const unsigned ai = P01[vi ? i : 0], ci = P2[vi ? i : 0];
+    const unsigned aiG = ai | G;
+    const int j0 = qj * 64 + qq * 16;
+    unsigned long long mine = 0ull;
+    unsigned acc = 0u;
+#pragma unroll 4
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u;
+      const bool vj = j < N;
+      const unsigned aj = P01[vj ? j : 0], cj = P2[vj ? j : 0];
+      const bool ne = (ai != aj) | (ci != cj);
+      const bool le_ij = ((((aj | G) - ai) & G) == G) & (ci <= cj);  // r(i) <= r(j)
+      const bool le_ji = (((aiG - aj) & G) == G) & (cj <= ci);
+      const unsigned long long m = __ballot(vi && vj && ne && le_ij);
+      mine = lane == u ? m : mine;
+      acc |= (vi && vj && ne && le_ji) ? (1u << u) : 0u;
+    }
+    if (lane < 16 && j0 + lane < N) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
+    if (qi != qj && i < N) dom16[((size_t)i * NW + qj) * 4 + qq] = (unsigned short)acc;
   }
 }
 
@@ -457,6 +651,9 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   PHASE(0)
 
   // ---- load merged F, ref points
+  constexpr bool RANKDOM = MV_DOM_RANKS && NWMAX * 64 > SURV_NLDS;
+  static_assert(!RANKDOM || T / 64 <= 13, "per-wave NaN flags live in iscal[0, 13)");
+  bool any_nan = false;
   for (int m = tid; m < N; m += T) {
     int s = m;
     const double* src;
@@ -467,13 +664,17 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     } else {
       src = a.F + ((size_t)b * N + m) * 3;
     }
-    L.F[m * 3 + 0] = src[0];
-    L.F[m * 3 + 1] = src[1];
-    L.F[m * 3 + 2] = src[2];
+    const double f0 = src[0], f1 = src[1], f2 = src[2];
+    L.F[m * 3 + 0] = f0;
+    L.F[m * 3 + 1] = f1;
+    L.F[m * 3 + 2] = f2;
+    any_nan |= (f0 != f0) | (f1 != f1) | (f2 != f2);
     L.slot[m] = s;
     L.front_of[m] = -1;
     L.sel[m] = 0;
   }
+  // per-wave NaN flags (iscal[0, T / 64)): the rank dominance needs a total order
+  if (RANKDOM && lane == 0) L.iscal[wave] = __ballot(any_nan) != 0ull;
   for (int m = N + tid; m < NW * 64; m += T) {  // padding rows: compare false both ways
     L.F[m * 3 + 0] = __builtin_nan("");
     L.F[m * 3 + 1] = __builtin_nan("");
@@ -487,6 +688,17 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   }
   __syncthreads();
   PHASE(1)
+  // ---- (N > SURV_NLDS, no NaN objective) per-objective ranks as packed words, in the
+  // niching temporaries (free until the niching; surv_offsets reserves the space)
+  bool rank_dom = false;
+  unsigned* P01 = (unsigned*)(smem + o.count);
+  unsigned* P2 = P01 + RANK_N2;
+  if constexpr (RANKDOM) {
+    bool nan_rows = false;
+    for (int w = 0; w < T / 64; ++w) nan_rows |= L.iscal[w] != 0;
+    rank_dom = !nan_rows;
+    if (rank_dom) rank_words<T>(L.F, N, (int*)(P2 + RANK_N2), P01, P2, L.iscal + 16);
+  }
 
   // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: wave
   // 0, before it joins the dominance pass below (independent of it; its results are first
@@ -546,7 +758,9 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   // ballot is word qi of dom[j], kept by lane u); gt && !lt -> j dominates
   // i, bit u of this lane's 16-bit quarter qq of word qj of dom[i] (off-diagonal pairs
   // only: the diagonal block is covered by its ballots).
-  {
+  if (RANKDOM && rank_dom) {
+    dominance_items_ranks(L, N, NW, lane, P01, P2);
+  } else {
     unsigned short* dom16 = (unsigned short*)L.dom;
     const int n_q = NW * (NW + 1) * 2;  // block pairs x 4 quarters
     for (;;) {
@@ -731,72 +945,71 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     __syncthreads();
     PHASE(22)
-    double ex[9], wfr[3];
-    for (int i = 0; i < 3; ++i) {
-      double v = L.red[i];
-      int ix = (int)L.red[3 + i];
-      double w = L.red[6 + i];
-      for (int ww = 1; ww < T / 64; ++ww) {
-        const double ov = L.red[ww * 16 + i];
-        const int oi = (int)L.red[ww * 16 + 3 + i];
-        if (ov < v || (ov == v && oi < ix)) {
-          v = ov;
-          ix = oi;
-        }
-        w = max_prop(w, L.red[ww * 16 + 6 + i]);
-      }
-      wfr[i] = w;
-      double row[3];
-      if (ix < ne) {
-        for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
-      } else if (ix < ne + n0) {
-        const int m = L.I[ix - ne];
-        for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
-      } else {
-        for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
-      }
-      for (int k = 0; k < 3; ++k) ex[i * 3 + k] = row[k];
-    }
-    // nadir (get_nadir_point with the call-site argument swap), in every wave
-    double idl[3];
-    for (int k = 0; k < 3; ++k) idl[k] = ideal[k];
-    double M[3][3], plane[3] = {1.0, 1.0, 1.0};
-    for (int i = 0; i < 3; ++i)
-      for (int k = 0; k < 3; ++k) M[i][k] = ex[i * 3 + k] - idl[k];
-    double Mc[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
-    bool ok = lu_solve3(Mc, plane);
-    double nd[3];
-    if (ok) {
-      double icp[3];
-      for (int k = 0; k < 3; ++k) {
-        icp[k] = 1.0 / plane[k];
-        nd[k] = idl[k] + icp[k];
-      }
-      bool close = true, small = false;
-      for (int i = 0; i < 3; ++i) {
-        const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
-        close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
-        small = small || (icp[i] <= 1e-6);
-      }
-      if (!close || small) {
-        ok = false;
-      } else {
-        for (int k = 0; k < 3; ++k)
-          if (nd[k] > worst[k]) nd[k] = worst[k];
-      }
-    }
-    if (!ok)
-      for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
-    for (int k = 0; k < 3; ++k)
-      if (nd[k] - idl[k] <= 1e-6) nd[k] = wfr[k];
-    // every wave writes the same values; each wave reads back only what it wrote itself
-    // (LDS is in order within a wave) until the next barrier
+    // lane 0 of every wave: the same combination and nadir, written to the same LDS words
+    // (identical bits); a wave reads back only what it wrote itself (LDS is in order within
+    // a wave) until the next barrier.  (Computed by one lane, in the shape of a single-
+    // thread block, the kernel keeps its register count: 79 VGPRs, 3 workgroups per CU.)
     if (lane == 0) {
-      for (int k = 0; k < 9; ++k) ext[k] = ex[k];
+      for (int i = 0; i < 3; ++i) {
+        double v = L.red[i];
+        int ix = (int)L.red[3 + i];
+        double w = L.red[6 + i];
+        for (int ww = 1; ww < T / 64; ++ww) {
+          const double ov = L.red[ww * 16 + i];
+          const int oi = (int)L.red[ww * 16 + 3 + i];
+          if (ov < v || (ov == v && oi < ix)) {
+            v = ov;
+            ix = oi;
+          }
+          w = max_prop(w, L.red[ww * 16 + 6 + i]);
+        }
+        wfront[i] = w;
+        double row[3];
+        if (ix < ne) {
+          for (int k = 0; k < 3; ++k) row[k] = pext[ix * 3 + k];
+        } else if (ix < ne + n0) {
+          const int m = L.I[ix - ne];
+          for (int k = 0; k < 3; ++k) row[k] = L.F[m * 3 + k];
+        } else {
+          for (int k = 0; k < 3; ++k) row[k] = L.ref[(ix - ne - n0) * 3 + k];
+        }
+        for (int k = 0; k < 3; ++k) ext[i * 3 + k] = row[k];
+      }
+    }
+    wave_sync();
+    if (lane == 0) {
+      // nadir (get_nadir_point with the call-site argument swap)
+      double M[3][3], plane[3] = {1.0, 1.0, 1.0};
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) M[i][k] = ext[i * 3 + k] - ideal[k];
+      double Mc[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) Mc[i][k] = M[i][k];
+      bool ok = lu_solve3(Mc, plane);
+      double nd[3];
+      if (ok) {
+        double icp[3];
+        for (int k = 0; k < 3; ++k) {
+          icp[k] = 1.0 / plane[k];
+          nd[k] = ideal[k] + icp[k];
+        }
+        bool close = true, small = false;
+        for (int i = 0; i < 3; ++i) {
+          const double mp = (M[i][0] * plane[0] + M[i][1] * plane[1]) + M[i][2] * plane[2];
+          close = close && (fabs(mp - 1.0) <= 1e-8 + 1e-5 * 1.0);
+          small = small || (icp[i] <= 1e-6);
+        }
+        if (!close || small) {
+          ok = false;
+        } else {
+          for (int k = 0; k < 3; ++k)
+            if (nd[k] > worst[k]) nd[k] = worst[k];
+        }
+      }
+      if (!ok)
+        for (int k = 0; k < 3; ++k) nd[k] = wpop[k];
       for (int k = 0; k < 3; ++k) {
-        wfront[k] = wfr[k];
+        if (nd[k] - ideal[k] <= 1e-6) nd[k] = wfront[k];
         nadir[k] = nd[k];
       }
     }
@@ -835,7 +1048,11 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
       const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
       for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
+#if MV_ASSOC_F64
+      ((double4*)L.Uf)[r] = make_double4(L.U[r * 3], L.U[r * 3 + 1], L.U[r * 3 + 2], 0.0);
+#else
       L.Uf[r] = make_float4((float)L.U[r * 3], (float)L.U[r * 3 + 1], (float)L.U[r * 3 + 2], 0.f);
+#endif
     }
     if (tid == 0) L.iscal[15] = 0;
     __syncthreads();
@@ -856,6 +1073,127 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     // the sequential scan).
     const int nh = RN >> 1;  // directions per half (wave-uniform loop counts); an odd RN's
                              // last direction goes to the second half's chain 0
+#if MV_ASSOC_F64
+    for (int v = tid; v < 2 * n_ranked; v += T) {
+      const int p = v >> 1, hf = v & 1;
+      const int jb = hf ? nh : 0;
+      const bool odd = hf && (RN & 1);
+      const int m = L.I[p];
+      double Nn[3];
+      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
+      if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
+          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0 (both lanes)
+        if (!hf) {
+          L.niche[p] = 0;
+          L.dist[p] = 0.0;
+        }
+        continue;
+      }
+      // fp64 pre-filter of the squared perpendicular distances, |N|^2 - (N.u)^2 with FMAs on
+      // the same unit directions as the exact pass.  Its error against the exact pass's
+      // sqrt'ed value squared is below 20 u |N|^2 (u = 2^-53: the dot product 3 u |N|, its
+      // square 6 u |N|^2, |N|^2 3 u |N|^2; the exact pass's own e = s u - N error 10 u |N| |e|),
+      // so the exact minimum -- and every direction whose sqrt'ed distance ties it -- lies
+      // within tol = 1e-14 (|N|^2 + best) > 40 u |N|^2 + 4.5e-16 best of the pre-filter's
+      // minimum.  Unlike the fp32 filter's 3e-5 |N|^2 this separates crowded directions
+      // (late botnet generations), so no refinement sweeps are needed; more than four hits
+      // (near-duplicate directions) or a NaN / overflow go to the exact pass below.
+      const double nn = fma(Nn[0], Nn[0], fma(Nn[1], Nn[1], Nn[2] * Nn[2]));
+      const double4* Ud = (const double4*)L.Uf;
+      auto d2f = [&](int j) {
+        const double4 u = Ud[j];
+        const double sp = fma(Nn[0], u.x, fma(Nn[1], u.y, Nn[2] * u.z));
+        return fma(-sp, sp, nn);
+      };
+      double b0 = __builtin_inf(), b1 = b0, b2 = b0, b3 = b0;
+      const int n4 = nh >> 2;
+      if (nn < __builtin_inf()) {
+#pragma unroll MV_ASSOC_UNROLL
+        for (int k = 0; k < n4; ++k) {
+          const int j = jb + 4 * k;
+          b0 = __builtin_fmin(b0, d2f(j));
+          b1 = __builtin_fmin(b1, d2f(j + 1));
+          b2 = __builtin_fmin(b2, d2f(j + 2));
+          b3 = __builtin_fmin(b3, d2f(j + 3));
+        }
+        for (int j = jb + 4 * n4; j < jb + nh; ++j) b0 = __builtin_fmin(b0, d2f(j));
+        if (odd) b0 = __builtin_fmin(b0, d2f(RN - 1));
+      }
+      double best = __builtin_fmin(__builtin_fmin(b0, b1), __builtin_fmin(b2, b3));
+      best = __builtin_fmin(best, __shfl_xor(best, 1, 64));
+      const double lim = best + 1e-14 * (nn + best);
+      if (lim < __builtin_inf()) {  // false on NaN / inf (the same in both lanes)
+        double bd = __builtin_inf();
+        int bj = 0;
+        auto cand = [&](int j) {  // exact fp64 distance, np.argmin order
+          const double* u = &L.U[j * 3];
+          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
+          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
+          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
+          if (arg_better(dd, j, bd, bj)) {
+            bd = dd;
+            bj = j;
+          }
+        };
+        const unsigned cm0 = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) |
+                             (b2 <= lim ? 4u : 0u) | (b3 <= lim ? 8u : 0u);
+        int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
+        auto hit = [&](int jc) {
+          c0 = nc == 0 ? jc : c0;
+          c1 = nc == 1 ? jc : c1;
+          c2 = nc == 2 ? jc : c2;
+          c3 = nc == 3 ? jc : c3;
+          ++nc;
+        };
+        unsigned cm = cm0;
+        while (cm) {  // every direction of this half within lim, in chain order
+          const int u = __builtin_ctz(cm);
+          cm &= cm - 1u;
+          int k = 0;
+          for (; k + 4 <= n4; k += 4) {
+            const int jc = jb + 4 * k + u;
+            const double d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
+            if (d0 <= lim) hit(jc);
+            if (d1 <= lim) hit(jc + 4);
+            if (d2 <= lim) hit(jc + 8);
+            if (d3 <= lim) hit(jc + 12);
+          }
+          for (; k < n4; ++k) {
+            const int jc = jb + 4 * k + u;
+            if (d2f(jc) <= lim) hit(jc);
+          }
+          if (u == 0) {
+            for (int jc = jb + 4 * n4; jc < jb + nh; ++jc)
+              if (d2f(jc) <= lim) hit(jc);
+            if (odd && d2f(RN - 1) <= lim) hit(RN - 1);
+          }
+        }
+        const bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;
+        if (!ovf) {
+          if (nc > 0) cand(c0);
+          if (nc > 1) cand(c1);
+          if (nc > 2) cand(c2);
+          if (nc > 3) cand(c3);
+        }
+        const double od = __shfl_xor(bd, 1, 64);
+        const int oj = __shfl_xor(bj, 1, 64);
+        if (arg_better(od, oj, bd, bj)) {
+          bd = od;
+          bj = oj;
+        }
+        if (!hf) {
+          if (ovf) {
+            L.key[atomicAdd(&L.iscal[15], 1)] = p;
+          } else {
+            L.niche[p] = bj;
+            L.dist[p] = bd;
+          }
+        }
+      } else if (!hf) {
+        L.key[atomicAdd(&L.iscal[15], 1)] = p;
+      }
+    }
+#else
     for (int v = tid; v < 2 * n_ranked; v += T) {
       const int p = v >> 1, hf = v & 1;
       const int jb = hf ? nh : 0;
@@ -1022,6 +1360,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         L.key[atomicAdd(&L.iscal[15], 1)] = p;
       }
     }
+#endif
     __syncthreads();
     PHASE(10)
     // exact np.argmin over sqrt'ed distances for the flagged individuals: one individual per
@@ -1310,9 +1649,12 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
                plan ? (int*)L.sortk : nullptr);
   }
   __syncthreads();
-  if (plan) {
-    variation_plan<T>(a, b, sel_gen, (const int*)L.sortk, pgeo, pcmap, pginfo);
+  if (plan) {  // (clocks: slots 23 / 24 bracket the plan of the last generation that has one)
+    PHASE(23)
+    variation_plan<T>(a, b, sel_gen, (const int*)L.sortk, (int*)L.sortk + 2 * n_m_next, pgeo,
+                      pcmap, pginfo);
     __syncthreads();
+    PHASE(24)
   }
   PHASE(9)
 #undef PHASE

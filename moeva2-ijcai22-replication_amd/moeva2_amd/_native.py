@@ -123,7 +123,10 @@ def lib():
             "mv_set_gene_layout": [vp, _i32p, C.c_int32],
         }
         for name, args in sig.items():
-            fn = getattr(L, name)
+            try:
+                fn = getattr(L, name)
+            except AttributeError:  # an older build (A/B runs): the call itself will fail
+                continue
             fn.argtypes = args
             fn.restype = C.c_int
         L.mv_engine_destroy.argtypes = [vp]
