@@ -442,7 +442,9 @@ __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, c
   }
 }
 
-// ---- N > SURV_NLDS: dominance from per-objective ranks (MV_DOM_RANKS, default on).
+// ---- N > SURV_NLDS: dominance from per-objective ranks (MV_DOM_RANKS, default OFF: round 5
+// A/B at configs[3], 20 generations: k_survive 135.4 ms per launch with it vs 91.7 ms with the
+// six-compare pass, 206 vs 278 M evals/s, profiles/r05/ab_survival/; bit-identical either way).
 // r_k(i) = #{j : F_k(j) < F_k(i)} preserves every <, = and > between the values of
 // objective k when none is NaN, so i dominates j (every F_k(i) <= F_k(j), one <) exactly
 // when every r_k(i) <= r_k(j) and the rank triples differ.  The ranks come from three
@@ -453,7 +455,7 @@ __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, c
 // 15 and 31: (P01j | G) - P01i keeps guard k iff r_k(j) >= r_k(i)) plus one u32 compare for
 // r2 -- 32-bit integer operations instead of six fp64 compares per pair.
 #ifndef MV_DOM_RANKS
-#define MV_DOM_RANKS 1
+#define MV_DOM_RANKS 0
 #endif
 constexpr int RANK_N2 = 1024;  // padded sort length (N <= SURV_NMAX)
 
