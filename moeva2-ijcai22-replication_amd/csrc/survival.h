@@ -181,9 +181,6 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(dmin, (size_t)RN * 8)
   TAKE(lround, (size_t)(2 * N + 2) * 4)
   unsigned total = alias ? end : off;
-  // N > SURV_NLDS: the rank dominance's words and sort indices (5 RANK_N2 u32) in the
-  // niching temporaries (appended there: the bitsets live in HBM)
-  if (!dom_lds && total < o.count + 5u * 1024u * 4u) total = o.count + 5u * 1024u * 4u;
   if (ptab_words > 0 && (size_t)ptab_words * 4 > (size_t)NW * 64 * 3 * 8) {
     off = total;
     TAKE(ptab, (size_t)ptab_words * 4)
@@ -442,150 +439,6 @@ __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, c
   }
 }
 
-// ---- N > SURV_NLDS: dominance from per-objective ranks (MV_DOM_RANKS, default OFF: round 5
-// A/B at configs[3], 20 generations: k_survive 135.4 ms per launch with it vs 91.7 ms with the
-// six-compare pass, 206 vs 278 M evals/s, profiles/r05/ab_survival/; bit-identical either way).
-// r_k(i) = #{j : F_k(j) < F_k(i)} preserves every <, = and > between the values of
-// objective k when none is NaN, so i dominates j (every F_k(i) <= F_k(j), one <) exactly
-// when every r_k(i) <= r_k(j) and the rank triples differ.  The ranks come from three
-// bitonic sorts of the individuals' indices (by value, then index; all three objectives in
-// every stage) and a max-scan of the sorted runs' starts -- O(N log^2 N) instead of the
-// O(N^2) counting of round 4 (whose cost matched the pair pass it replaced).  The pair pass
-// then tests two 16-bit fields with guards in one u32 (P01 = r0 | r1 << 16, guards at bits
-// 15 and 31: (P01j | G) - P01i keeps guard k iff r_k(j) >= r_k(i)) plus one u32 compare for
-// r2 -- 32-bit integer operations instead of six fp64 compares per pair.
-#ifndef MV_DOM_RANKS
-#define MV_DOM_RANKS 0
-#endif
-constexpr int RANK_N2 = 1024;  // padded sort length (N <= SURV_NMAX)
-
-// Sorted index arrays idx[k * RANK_N2 + p] of objective k (ascending value, ties by index,
-// the padding indices >= N last), then ranks into P01 / P2 (u32 words).  All threads; ends
-// on a barrier.  wsum: one int per wave.
-template <int T>
-__device__ __forceinline__ void rank_words(const double* F, const int N, int* idx,
-                                           unsigned* P01, unsigned* P2, int* wsum) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int n2 = RANK_N2, h = RANK_N2 / 2;
-  for (int t = tid; t < 3 * n2; t += T) idx[t] = t & (n2 - 1);
-  __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = tid; t < 3 * h; t += T) {
-        const int k = t / h, tt = t - k * h;
-        const int i = 2 * tt - (tt & (stride - 1));
-        const int j = i + stride;
-        int* ik = idx + k * n2;
-        const int x = ik[i], y = ik[j];
-        bool gt;  // (value, index) of x > that of y; padding indices sort last
-        if (x >= N || y >= N) {
-          gt = (x >= N && y >= N) ? x > y : x >= N;
-        } else {
-          const double vx = F[x * 3 + k], vy = F[y * 3 + k];
-          gt = vx > vy || (vx == vy && x > y);
-        }
-        if (gt == ((i & size) == 0)) {
-          ik[i] = y;
-          ik[j] = x;
-        }
-      }
-      __syncthreads();
-    }
-  // rank of the individual at sorted position q = the start of its run of equal values:
-  // an inclusive max-scan of (q if the value differs from position q - 1, else 0)
-  constexpr int PER = n2 / T;  // positions per thread and objective (contiguous)
-  int rk[3][PER];
-  for (int k = 0; k < 3; ++k) {
-    const int* ik = idx + k * n2;
-    int run = 0;
-    for (int e = 0; e < PER; ++e) {
-      const int q = tid * PER + e;
-      int st = 0;
-      if (q < N) {
-        const int x = ik[q];
-        st = (q == 0 || F[ik[q - 1] * 3 + k] != F[x * 3 + k]) ? q : 0;
-      }
-      run = st > run ? st : run;
-      rk[k][e] = run;
-    }
-    // exclusive max over the threads before this one: wave scan, then the waves' totals
-    int incl = run;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl = y > incl ? y : incl;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int before = __shfl_up(incl, 1, 64);
-    if (lane == 0) before = 0;
-    for (int w = 0; w < wave; ++w) before = wsum[w] > before ? wsum[w] : before;
-    for (int e = 0; e < PER; ++e) rk[k][e] = rk[k][e] > before ? rk[k][e] : before;
-    __syncthreads();  // wsum is reused by the next objective
-  }
-  for (int e = 0; e < PER; ++e) {
-    const int q = tid * PER + e;
-    if (q < N) {
-      P01[idx[q]] = 0u;  // fields below are ORed in by objective
-    }
-  }
-  __syncthreads();
-  for (int k = 0; k < 3; ++k)
-    for (int e = 0; e < PER; ++e) {
-      const int q = tid * PER + e;
-      if (q < N) {
-        const int x = idx[k * n2 + q];
-        if (k == 0) atomicOr(&P01[x], (unsigned)rk[0][e]);
-        if (k == 1) atomicOr(&P01[x], (unsigned)rk[1][e] << 16);
-        if (k == 2) P2[x] = (unsigned)rk[2][e];
-      }
-    }
-  __syncthreads();
-}
-
-// The dominance work items of the six-compare pass on the rank words: the same bits.
-__device__ __forceinline__ void dominance_items_ranks(SurvLds& L, const int N, const int NW,
-                                                      const int lane, const unsigned* P01,
-                                                      const unsigned* P2) {
-  unsigned short* dom16 = (unsigned short*)L.dom;
-  constexpr unsigned G = 0x80008000u;
-  const int n_q = NW * (NW + 1) * 2;
-  for (;;) {
-    int t = 0;
-    if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
-    t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
-    if (t >= n_q) break;
-    const int qq = t & 3;
-    int qi = 0, rem = t >> 2;
-    while (rem >= NW - qi) {
-      rem -= NW - qi;
-      ++qi;
-    }
-    const int qj = qi + rem;
-    const int i = qi * 64 + lane;
-    const bool vi = i < N;
-    const unsigned ai = P01[vi ? i : 0], ci = P2[vi ? i : 0];
-    const unsigned aiG = ai | G;
-    const int j0 = qj * 64 + qq * 16;
-    unsigned long long mine = 0ull;
-    unsigned acc = 0u;
-#pragma unroll 4
-    for (int u = 0; u < 16; ++u) {
-      const int j = j0 + u;
-      const bool vj = j < N;
-      const unsigned aj = P01[vj ? j : 0], cj = P2[vj ? j : 0];
-      const bool ne = (ai != aj) | (ci != cj);
-      const bool le_ij = ((((aj | G) - ai) & G) == G) & (ci <= cj);  // r(i) <= r(j)
-      const bool le_ji = (((aiG - aj) & G) == G) & (cj <= ci);
-      const unsigned long long m = __ballot(vi && vj && ne && le_ij);
-      mine = lane == u ? m : mine;
-      acc |= (vi && vj && ne && le_ji) ? (1u << u) : 0u;
-    }
-    if (lane < 16 && j0 + lane < N) L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
-    if (qi != qj && i < N) dom16[((size_t)i * NW + qj) * 4 + qq] = (unsigned short)acc;
-  }
-}
-
 // NWMAX: dominance words per individual held in registers (N <= 64 NWMAX); above
 // SURV_NLDS the bitsets go to the HBM scratch a.dom_g instead of LDS.
 // a: pointers and sizes (slot or dense mode); b: the state; N, gen, sel_gen and
@@ -653,9 +506,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   PHASE(0)
 
   // ---- load merged F, ref points
-  constexpr bool RANKDOM = MV_DOM_RANKS && NWMAX * 64 > SURV_NLDS;
-  static_assert(!RANKDOM || T / 64 <= 13, "per-wave NaN flags live in iscal[0, 13)");
-  bool any_nan = false;
   for (int m = tid; m < N; m += T) {
     int s = m;
     const double* src;
@@ -670,13 +520,10 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     L.F[m * 3 + 0] = f0;
     L.F[m * 3 + 1] = f1;
     L.F[m * 3 + 2] = f2;
-    any_nan |= (f0 != f0) | (f1 != f1) | (f2 != f2);
     L.slot[m] = s;
     L.front_of[m] = -1;
     L.sel[m] = 0;
   }
-  // per-wave NaN flags (iscal[0, T / 64)): the rank dominance needs a total order
-  if (RANKDOM && lane == 0) L.iscal[wave] = __ballot(any_nan) != 0ull;
   for (int m = N + tid; m < NW * 64; m += T) {  // padding rows: compare false both ways
     L.F[m * 3 + 0] = __builtin_nan("");
     L.F[m * 3 + 1] = __builtin_nan("");
@@ -690,17 +537,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   }
   __syncthreads();
   PHASE(1)
-  // ---- (N > SURV_NLDS, no NaN objective) per-objective ranks as packed words, in the
-  // niching temporaries (free until the niching; surv_offsets reserves the space)
-  bool rank_dom = false;
-  unsigned* P01 = (unsigned*)(smem + o.count);
-  unsigned* P2 = P01 + RANK_N2;
-  if constexpr (RANKDOM) {
-    bool nan_rows = false;
-    for (int w = 0; w < T / 64; ++w) nan_rows |= L.iscal[w] != 0;
-    rank_dom = !nan_rows;
-    if (rank_dom) rank_words<T>(L.F, N, (int*)(P2 + RANK_N2), P01, P2, L.iscal + 16);
-  }
 
   // ---- ideal / worst (np.min/np.max over vstack(prev, F, ref)), worst of population: wave
   // 0, before it joins the dominance pass below (independent of it; its results are first
@@ -751,17 +587,50 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   }
   PHASE(11)
 
-  // ---- dominance bitsets: dom[j] bit i  <=>  i dominates j.  Work items are the unordered
-  // 64x64 block pairs (qi <= qj) split into the four 16-row quarters of block qj, taken
-  // from an LDS counter (wave 0 joins after ideal/worst).  Lane l holds row i = 64 qi + l;
+  // ---- dominance bitsets, word-major: bit i - 64 q of dom[q N + j]  <=>  i dominates j
+  // (lanes j read and write consecutive words).  Work items are the unordered 64x64 block
+  // pairs (qi <= qj) split into the four 16-row quarters of block qj, taken from an LDS
+  // counter (wave 0 joins after ideal/worst).  Lane l holds row i = 64 qi + l;
   // the 16 rows j of the quarter are LDS broadcasts, fully unrolled (F is padded to whole
   // blocks with NaN rows, which compare false both ways: no bounds tests).  One pass of
   // the six compares per (i, j) gives both directions: lt && !gt -> i dominates j (the
   // ballot is word qi of dom[j], kept by lane u); gt && !lt -> j dominates
   // i, bit u of this lane's 16-bit quarter qq of word qj of dom[i] (off-diagonal pairs
   // only: the diagonal block is covered by its ballots).
-  if (RANKDOM && rank_dom) {
-    dominance_items_ranks(L, N, NW, lane, P01, P2);
+  if (NWMAX * 64 > SURV_NLDS) {
+    // HBM bitsets: whole 64 x 64 block pairs, so both directions leave as full words in
+    // the word-major layout (dom[q N + j]): lane u's ballot word qi of dom[j0 + u] and lane
+    // l's 64-bit word qj of dom[i] are 512 contiguous bytes each (the quarter items' 2-byte
+    // stores to rows 128 B apart cost 28.8 GB of HBM traffic per configs[3] launch)
+    const int n_b = NW * (NW + 1) / 2;
+    for (;;) {
+      int t = 0;
+      if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
+      t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+      if (t >= n_b) break;
+      int qi = 0, rem = t;
+      while (rem >= NW - qi) {
+        rem -= NW - qi;
+        ++qi;
+      }
+      const int qj = qi + rem;
+      const int i = qi * 64 + lane;
+      const double fi0 = L.F[i * 3 + 0], fi1 = L.F[i * 3 + 1], fi2 = L.F[i * 3 + 2];
+      const int j0 = qj * 64;
+      const double* fj = L.F + j0 * 3;
+      unsigned long long mine = 0ull, acc = 0ull;
+#pragma unroll 4
+      for (int u = 0; u < 64; ++u) {
+        const double g0 = fj[u * 3], g1 = fj[u * 3 + 1], g2 = fj[u * 3 + 2];
+        const bool lt = (fi0 < g0) | (fi1 < g1) | (fi2 < g2);
+        const bool gt = (fi0 > g0) | (fi1 > g1) | (fi2 > g2);
+        const unsigned long long m = __ballot(lt && !gt);
+        mine = lane == u ? m : mine;
+        acc |= (gt && !lt) ? (1ull << u) : 0ull;
+      }
+      if (j0 + lane < N) L.dom[(size_t)qi * N + j0 + lane] = mine;
+      if (qi != qj && i < N) L.dom[(size_t)qj * N + i] = acc;
+    }
   } else {
     unsigned short* dom16 = (unsigned short*)L.dom;
     const int n_q = NW * (NW + 1) * 2;  // block pairs x 4 quarters
@@ -793,8 +662,8 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         acc |= (gt && !lt) ? (1u << u) : 0u;
       }
       if (lane < 16 && j0 + lane < N)
-        L.dom[(size_t)(j0 + lane) * NW + qi] = mine;
-      if (qi != qj && i < N) dom16[((size_t)i * NW + qj) * 4 + qq] = (unsigned short)acc;
+        L.dom[(size_t)qi * N + j0 + lane] = mine;
+      if (qi != qj && i < N) dom16[((size_t)qj * N + i) * 4 + qq] = (unsigned short)acc;
     }
   }
   __syncthreads();
@@ -806,7 +675,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       N,
       [&](int j) {
         for (int q = 0; q < NW; ++q)
-          if (L.dom[(size_t)j * NW + q]) return false;
+          if (L.dom[(size_t)q * N + j]) return false;
         return true;
       },
       L.I, 0, wsum);
@@ -829,7 +698,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         [&](int j) {
           if ((L.ranked[j >> 6] >> (j & 63)) & 1ull) return false;
           for (int q = 0; q < NW; ++q)
-            if (L.dom[(size_t)j * NW + q] & ~L.ranked[q]) return false;
+            if (L.dom[(size_t)q * N + j] & ~L.ranked[q]) return false;
           return true;
         },
         L.memb, 0, wsum);
@@ -838,7 +707,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       const int j = L.memb[k];
       int mx = -1;
       for (int q = 0; q < NW; ++q) {
-        unsigned long long bits = L.dom[(size_t)j * NW + q] & L.cur[q];
+        unsigned long long bits = L.dom[(size_t)q * N + j] & L.cur[q];
         while (bits) {
           const int i = q * 64 + __ffsll((long long)bits) - 1;
           bits &= bits - 1ull;
