@@ -186,16 +186,19 @@ def cpu_cores():
     return n
 
 
-def cpu_baseline(w, sample_gens=100, cores=None):
+def cpu_baseline(w, sample_gens=None, cores=None, states_per_core=2):
     """The oracle's CPU statement of the same loop (eval + survival + variation, numpy):
-    one process per host core, one initial state per process (like the reference's
-    joblib pool over states, n_jobs = cores), a bounded sample of generations."""
+    one process per host core (like the reference's joblib pool over states, n_jobs =
+    cores), a bounded sample of the workload -- states_per_core whole attacks per core at
+    the workload's generation budget (about 10 s of CPU work for botnet)."""
     from multiprocessing import get_context
 
     cores = cores or cpu_cores()
+    sample_gens = sample_gens or w["n_gen"]
     P, O = w["n_pop"] + 3, w["n_off"]
+    n_states = states_per_core * cores
     jobs = [(s, w["n_pop"], w["n_off"], sample_gens, w["norm"], w["history"])
-            for s in range(cores)]
+            for s in range(n_states)]
     with get_context("spawn").Pool(cores, initializer=_cpu_init,
                                    initargs=(w["project"],)) as pool:
         pool.map(_cpu_noop, range(4 * cores))  # every worker started and initialised
@@ -203,7 +206,7 @@ def cpu_baseline(w, sample_gens=100, cores=None):
         n_eval = sum(pool.map(_cpu_state, jobs, chunksize=1))
         dt = time.perf_counter() - t0
     return {"value": n_eval / dt, "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": f"{cores} {w['project']} states x {sample_gens} generations "
+            "sample": f"{n_states} {w['project']} states x {sample_gens} generations "
                       f"(P={P}, O={O}) of oracle/moeva_oracle.run_attack (numpy), one "
                       f"process per core; affinity mask {cpu_affinity()} CPUs, box CPU "
                       f"share (OMP_NUM_THREADS) {os.environ.get('OMP_NUM_THREADS', 'unset')}, "
@@ -223,7 +226,7 @@ def data_note(w, B):
     return f"{src[w['project']]} ({how}) + {clf} and shipped scaler"
 
 
-PROFILE_ROUNDS = ("r04", "r03", "r02")  # newest first: traffic measured on the current kernels wins
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: traffic measured on the current kernels wins
 
 
 def load_traffic(workload):
@@ -520,7 +523,9 @@ def main():
                          "(a separately labelled line: f1 is not Keras's value)")
     ap.add_argument("--shard", action="store_true",
                     help="strong scaling: split the states over the ranks")
-    ap.add_argument("--cpu-gens", type=int, default=300)
+    ap.add_argument("--cpu-gens", type=int, default=None,
+                    help="generations per state of the CPU baseline sample (default: the "
+                         "workload's budget)")
     args = ap.parse_args()
 
     if args.groups:

@@ -966,8 +966,10 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   // other groups' throughput-bound kernels.  Results do not depend on the grouping (every
   // draw is keyed by the row inside its state).  Profiling runs use one group so the
   // per-kernel event times are those of the kernels alone.
-  int ngrp = B / 64;  // about 100 states per group at the botnet size; capped at
-                      // MAX_GROUPS = 4 = GPU_MAX_HW_QUEUES (6 or 8 streams measured 35% slower)
+  int ngrp = B / 64;  // about 100 states per group at the botnet size; at most 4 =
+                      // GPU_MAX_HW_QUEUES (round 5: MV_GROUPS 6 / 8, with GPU_MAX_HW_QUEUES
+                      // 6 / 8: 148 / 147 vs 218 M evals/s; round 2: 35 % slower)
+  ngrp = ngrp > 4 ? 4 : ngrp;
   if (const char* g = std::getenv("MV_GROUPS")) ngrp = std::atoi(g);
   if (e->profiling) ngrp = 1;
   ngrp = ngrp < 1 ? 1 : (ngrp > MAX_GROUPS ? MAX_GROUPS : (ngrp > B ? B : ngrp));

@@ -48,7 +48,7 @@ constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P +
 constexpr int SURV_NLDS = 512;   // up to this N the dominance bitsets live in LDS, else in HBM
 constexpr int SURV_RMAX = 640;   // reference points
 constexpr int ARG_SLOTS = 32;    // constant-memory launch-argument slots per device
-constexpr int MAX_GROUPS = 4;    // state groups (streams) of one attack
+constexpr int MAX_GROUPS = 16;   // state groups (streams) of one attack (default 4: api.cpp)
 constexpr double INT_WIDEN = 0.5 - 1e-16;  // pymoo apply_float_operation bound widening
 
 struct DProblem {

@@ -281,31 +281,55 @@ __device__ __forceinline__ double wred_max(double v) {
   return wave_reduce(v, [](double a, double b) { return max_prop(a, b); });
 }
 // LAPACK dgetf2/dgetrs-order 3x3 solve (oracle lu_solve3).  Returns false if singular.
-__device__ inline bool lu_solve3(double A[3][3], double x[3]) {
+// Every array index is a compile-time constant after unrolling (the pivot row is swapped in
+// by selects, not by a runtime index), so A and x stay in registers: indexing them by the
+// pivot put both in scratch memory, ~10 k cycles of the nadir step per state.
+__device__ __forceinline__ bool lu_solve3(double (&A)[3][3], double (&x)[3]) {
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     int p = k;
-    for (int i = k + 1; i < 3; ++i)
-      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
-    if (A[p][k] == 0.0) return false;
-    if (p != k) {
+    double best = fabs(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < 3; ++i) {
+      const double v = fabs(A[i][k]);
+      if (v > best) {
+        best = v;
+        p = i;
+      }
+    }
+    double piv = A[k][k];
+#pragma unroll
+    for (int i = k + 1; i < 3; ++i) piv = p == i ? A[i][k] : piv;
+    if (piv == 0.0) return false;
+#pragma unroll
+    for (int i = k + 1; i < 3; ++i) {
+      const bool sw = p == i;
+#pragma unroll
       for (int j = 0; j < 3; ++j) {
         const double t = A[k][j];
-        A[k][j] = A[p][j];
-        A[p][j] = t;
+        A[k][j] = sw ? A[i][j] : t;
+        A[i][j] = sw ? t : A[i][j];
       }
       const double t = x[k];
-      x[k] = x[p];
-      x[p] = t;
+      x[k] = sw ? x[i] : t;
+      x[i] = sw ? t : x[i];
     }
     const double r = 1.0 / A[k][k];
+#pragma unroll
     for (int i = k + 1; i < 3; ++i) A[i][k] = A[i][k] * r;
+#pragma unroll
     for (int j = k + 1; j < 3; ++j)
+#pragma unroll
       for (int i = k + 1; i < 3; ++i) A[i][j] = A[i][j] - A[i][k] * A[k][j];
   }
+#pragma unroll
   for (int j = 0; j < 3; ++j)
+#pragma unroll
     for (int i = j + 1; i < 3; ++i) x[i] = x[i] - x[j] * A[i][j];
+#pragma unroll
   for (int j = 2; j >= 0; --j) {
     x[j] = x[j] / A[j][j];
+#pragma unroll
     for (int i = 0; i < j; ++i) x[i] = x[i] - x[j] * A[i][j];
   }
   return true;
