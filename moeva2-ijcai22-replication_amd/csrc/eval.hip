@@ -397,10 +397,13 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   // round trip is ~4 us, several rows' worth of work, and one row of prefetch left each row
   // waiting on its loads (r03 phase clocks: ~9.6 k cycles per row).  The first two rows'
   // loads go out before the mutation draws, whose gathers and pow chains then overlap them.
-  double xa[NT], xb[NT];
+  // MV_GENC_PF = 1: one row in flight instead of two (k_genc's register budget, A/B)
+  constexpr bool PF2 = !(EARLY && MV_GENC_PF == 1);
+  double xa[NT], xb[PF2 ? NT : 1];
   auto preload = [&]() {
     if (nrw > 0) load_row(0, xa);
-    if (nrw > 1) load_row(1, xb);
+    if constexpr (PF2)
+      if (nrw > 1) load_row(1, xb);
   };
   if (a.mode == 1) {
     if constexpr (PLAN)
@@ -506,12 +509,18 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   };
   for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
     double x[NT];
+    if constexpr (PF2) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      x[t] = xa[t];
-      xa[t] = xb[t];
+      for (int t = 0; t < NT; ++t) {
+        x[t] = xa[t];
+        xa[t] = xb[t];
+      }
+      if (k + 2 < nrw) load_row(k + 2, xb);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x[t] = xa[t];
+      if (k + 1 < nrw) load_row(k + 1, xa);
     }
-    if (k + 2 < nrw) load_row(k + 2, xb);
     if (sbx) {  // SBX children, then every mutation of the row
       const int i = rc.i0 + wave + VARY_W * k;
       const int nm = a.n / 2;

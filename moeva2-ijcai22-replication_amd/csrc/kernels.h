@@ -155,6 +155,11 @@ __host__ __device__ inline GenLds genc_early_lds(const VaryOff& o, const DProble
 #ifndef MV_GENC_FUSED
 #define MV_GENC_FUSED 1
 #endif
+// MV_GENC_PF: parent rows in flight ahead of the row k_genc's fused instance finishes (2; 1
+// for the register-budget A/B)
+#ifndef MV_GENC_PF
+#define MV_GENC_PF 2
+#endif
 __host__ __device__ inline GenLds genc_fused_lds(const VaryOff& o, const DProblem& p) {
   GenLds l{};
   const unsigned ssz = o.s_end - o.s_at;
