@@ -155,10 +155,10 @@ __host__ __device__ inline GenLds genc_early_lds(const VaryOff& o, const DProble
 #ifndef MV_GENC_FUSED
 #define MV_GENC_FUSED 1
 #endif
-// MV_GENC_PF: parent rows in flight ahead of the row k_genc's fused instance finishes (2; 1
-// for the register-budget A/B)
+// MV_GENC_PF: parent rows in flight ahead of the row k_genc's fused instance finishes: 1
+// (round 5: 220.6 vs 219.3 M evals/s with 2, k_genc 87.3 vs 89.3 us, no spilled registers)
 #ifndef MV_GENC_PF
-#define MV_GENC_PF 2
+#define MV_GENC_PF 1
 #endif
 __host__ __device__ inline GenLds genc_fused_lds(const VaryOff& o, const DProblem& p) {
   GenLds l{};
