@@ -44,6 +44,14 @@ constexpr int VARY_MAX_V = 1024;    // genes per row (16 per lane)
 #define MV_SURV_T 512
 #endif
 constexpr int SURV_T = MV_SURV_T;  // threads per survival workgroup (8 waves)
+// threads of the N > SURV_NLDS survival instance (configs[3], N = 963): 16 waves, so its
+// issue-bound dominance and association passes interleave four waves per SIMD (round 5:
+// k_survive 86.8 -> 70.2 ms per launch at configs[3]; 1024 threads at N = 303 measured
+// 110 vs 75 us, so the LDS-resident instance keeps SURV_T)
+#ifndef MV_SURV_T_BIG
+#define MV_SURV_T_BIG 1024
+#endif
+constexpr int SURV_T_BIG = MV_SURV_T_BIG;
 constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P + O = 963)
 constexpr int SURV_NLDS = 512;   // up to this N the dominance bitsets live in LDS, else in HBM
 constexpr int SURV_RMAX = 640;   // reference points

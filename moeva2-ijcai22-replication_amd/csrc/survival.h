@@ -126,6 +126,11 @@ struct SurvOff {
 // Round 4: 68.8 -> ~53 KiB per workgroup at N = 303, R = 200 (three workgroups per CU).
 // ptab_words: the variation plan's tables (geo, cmap, ginfo; 0 without a plan), staged after
 // survivor selection into the F rows when they fit (F is dead then), else appended.
+// Threads of the survival workgroup for N merged individuals (the kernel instance's T).
+__host__ __device__ __forceinline__ int surv_threads(int N) {
+  return N > SURV_NLDS ? SURV_T_BIG : SURV_T;
+}
+
 __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm,
                                                          int ptab_words = 0) {
   const bool dom_lds = N <= SURV_NLDS;
@@ -141,7 +146,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(U, (size_t)RN * 3 * 8)
   TAKE(Uf, (size_t)RN * (MV_ASSOC_F64 ? 32 : 16))
   TAKE(dist, (size_t)N * 8)
-  TAKE(red, (SURV_T / 64) * 16 * 8)
+  TAKE(red, (surv_threads(N) / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
   TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)

@@ -11,10 +11,11 @@
 
 namespace mv {
 
-template <int NWMAX>
-__global__ __launch_bounds__(SURV_T) void k_survive(SurvArgs a) {
+// T = surv_threads(N): SURV_T for the LDS-bitset instance, SURV_T_BIG above SURV_NLDS
+template <int NWMAX, int T>
+__global__ __launch_bounds__(T) void k_survive(SurvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  survive_state<NWMAX, SURV_T>(a, blockIdx.x, a.N, a.gen, a.sel_gen, a.parents_out, smem);
+  survive_state<NWMAX, T>(a, blockIdx.x, a.N, a.gen, a.sel_gen, a.parents_out, smem);
 }
 
 __global__ __launch_bounds__(SURV_T) void k_select(int P, int O, uint64_t seed, uint32_t sk,
@@ -95,18 +96,19 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
       surv_lds_bytes(a.N, a.R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0) + pad;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64>,
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64, SURV_T>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NMAX / 64>,
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NMAX / 64, SURV_T_BIG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     configured = true;
   }
   if (a.N <= SURV_NLDS) {
-    hipLaunchKernelGGL(k_survive<SURV_NLDS / 64>, dim3(B), dim3(SURV_T), lds, stream, a);
+    hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T>), dim3(B), dim3(SURV_T), lds, stream, a);
   } else {
     if (!a.dom_g || a.dom_stride < (size_t)a.N * ((a.N + 63) / 64)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_survive<SURV_NMAX / 64>, dim3(B), dim3(SURV_T), lds, stream, a);
+    hipLaunchKernelGGL((k_survive<SURV_NMAX / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
+                       stream, a);
   }
   return hipGetLastError();
 }
