@@ -870,8 +870,9 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   {
     const int n_m = (O + 1) / 2, pslots = ((n_m * 4 + P - 1) / P) * P;
     const int ptab = plan_tab_words(e->ap().Vr, e->ap().V);
-    if (surv_lds_bytes(P + O, R, pslots, ptab) > 160 * 1024 ||
-        surv_lds_bytes(P, R, pslots, ptab) > 160 * 1024)
+    if (surv_lds_bytes(P + O, R, pslots, ptab, P + O > SURV_NLDS ? SURV_T_BIG : SURV_T_MID) >
+            160 * 1024 ||
+        surv_lds_bytes(P, R, pslots, ptab, P > SURV_NLDS ? SURV_T_BIG : SURV_T_MID) > 160 * 1024)
       return fail(MV_ERR_ARG, "pop_size + n_offsprings and n_ref too large for the survival LDS");
   }
   hipStream_t stream = (hipStream_t)stream_;
@@ -1069,6 +1070,15 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
   sa.O_next = O;
   sa.dom_g = e->dom_g;
   sa.dom_stride = e->dom_stride;
+  {  // 10-wave survival workgroups when every state fits two workgroups per CU (SurvArgs.wide)
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+    (void)hipGetLastError();
+    sa.wide = B <= 2 * cus ? 1 : 0;
+    if (const char* w = std::getenv("MV_SURV_WIDE")) sa.wide = std::atoi(w);  // A/B
+  }
   if (use_plan) {
     const VaryOff vo = vary_offsets(ap);
     sa.plan_hdr = e->plan_hdr;

@@ -52,6 +52,14 @@ constexpr int SURV_T = MV_SURV_T;  // threads per survival workgroup (8 waves)
 #define MV_SURV_T_BIG 1024
 #endif
 constexpr int SURV_T_BIG = MV_SURV_T_BIG;
+// threads of the N <= SURV_NLDS instance when the attack's states all fit two workgroups per
+// CU (SurvArgs.wide): 10 waves (round 5, headline: 225.4 vs 220.2 M evals/s with 512; 768:
+// 224.8 M; 896: 200.6 M; with 4,000 states (configs[2]) 768 threads lose occupancy: 461.5 vs
+// 481.4 M, so many states keep SURV_T)
+#ifndef MV_SURV_T_MID
+#define MV_SURV_T_MID 640
+#endif
+constexpr int SURV_T_MID = MV_SURV_T_MID;
 constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P + O = 963)
 constexpr int SURV_NLDS = 512;   // up to this N the dominance bitsets live in LDS, else in HBM
 constexpr int SURV_RMAX = 640;   // reference points
@@ -236,6 +244,7 @@ struct SurvArgs {
   int Vr, V, n_sub0, n_sub1;
   double cx_prob;
   int cx_sbx;               // SBX: the subsets' mating-level draws only
+  int wide;                 // N <= SURV_NLDS: SURV_T_MID threads per state instead of SURV_T
 };
 
 // Stand-alone classifier forward (Classifier.predict_proba) -------------------------------

@@ -214,7 +214,7 @@ hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, cons
 // the returned slot, then release it on the same stream after the slot's last launch.
 hipError_t stage_rows(const RowsArgs& a, hipStream_t stream, int* slot);
 hipError_t release_rows(int slot, hipStream_t stream);
-size_t surv_lds_bytes(int N, int R, int P, int ptab_words = 0);
+size_t surv_lds_bytes(int N, int R, int P, int ptab_words = 0, int threads = 0);
 
 hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipStream_t stream);
 // Which kernels launch_gen / launch_cons run for these rows: 0 k_gen + k_cons, 1 k_narrow

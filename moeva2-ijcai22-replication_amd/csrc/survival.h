@@ -132,7 +132,7 @@ __host__ __device__ __forceinline__ int surv_threads(int N) {
 }
 
 __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm,
-                                                         int ptab_words = 0) {
+                                                         int ptab_words = 0, int threads = 0) {
   const bool dom_lds = N <= SURV_NLDS;
   const unsigned NW = (N + 63) / 64;
   const unsigned RN = R + 3;
@@ -146,7 +146,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(U, (size_t)RN * 3 * 8)
   TAKE(Uf, (size_t)RN * (MV_ASSOC_F64 ? 32 : 16))
   TAKE(dist, (size_t)N * 8)
-  TAKE(red, (surv_threads(N) / 64) * 16 * 8)
+  TAKE(red, ((threads ? threads : surv_threads(N)) / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
   TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)
@@ -482,7 +482,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   const int n_m_next = parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = parents_out ? ((n_m_next * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
   const bool plan = parents_out && a.plan_hdr;
-  const SurvOff o = surv_offsets(N, R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0);
+  const SurvOff o = surv_offsets(N, R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0, T);
   SurvLds L;
   L.F = (double*)(smem + o.F);
   L.ref = a.ref;  // global (surv_offsets)

@@ -83,8 +83,8 @@ hipError_t take_survival_dump(double* out) {
 #endif
 }
 
-size_t surv_lds_bytes(int N, int R, int Pperm, int ptab_words) {
-  return surv_offsets(N, R, Pperm, ptab_words).total;
+size_t surv_lds_bytes(int N, int R, int Pperm, int ptab_words, int threads) {
+  return surv_offsets(N, R, Pperm, ptab_words, threads).total;
 }
 
 hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
@@ -92,11 +92,14 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   const int n_m = a.parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = a.parents_out ? ((n_m * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
   static const size_t pad = lds_pad("MV_LDS_PAD_SURV");
+  const int T = a.N > SURV_NLDS ? SURV_T_BIG : (a.wide ? SURV_T_MID : SURV_T);
   const size_t lds =
-      surv_lds_bytes(a.N, a.R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0) + pad;
+      surv_lds_bytes(a.N, a.R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0, T) + pad;
   static bool configured = false;
   if (!configured) {
     (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64, SURV_T>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64, SURV_T_MID>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k_survive<SURV_NMAX / 64, SURV_T_BIG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -104,7 +107,12 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
     configured = true;
   }
   if (a.N <= SURV_NLDS) {
-    hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T>), dim3(B), dim3(SURV_T), lds, stream, a);
+    if (T == SURV_T_MID)
+      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T_MID>), dim3(B), dim3(SURV_T_MID), lds,
+                         stream, a);
+    else
+      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T>), dim3(B), dim3(SURV_T), lds, stream,
+                         a);
   } else {
     if (!a.dom_g || a.dom_stride < (size_t)a.N * ((a.N + 63) / 64)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_survive<SURV_NMAX / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
