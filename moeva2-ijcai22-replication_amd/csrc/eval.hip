@@ -1071,7 +1071,10 @@ template <int CJ, bool BF, bool DIRECT, bool CO>
 #ifndef MV_MLP2_OCC
 #define MV_MLP2_OCC 2  // fp32 gene-reading instance: minimum waves per SIMD
 #endif
-__global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? MV_MLP2_OCC : 1)) void k_mlp2(int slot, int hist_row0) {
+#ifndef MV_MLP2_OCC_XML
+X
+#endif
+__global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? MV_MLP2_OCC : MV_MLP2_OCC_XML)) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
   const DProblem& p = a.p;
