@@ -1071,8 +1071,11 @@ template <int CJ, bool BF, bool DIRECT, bool CO>
 #ifndef MV_MLP2_OCC
 #define MV_MLP2_OCC 2  // fp32 gene-reading instance: minimum waves per SIMD
 #endif
+// fp32 instances reading the ML rows (LCLD: k_narrow's xml): two waves per SIMD (222 VGPRs,
+// no AGPR spill; round 5: configs[2] 485.6 -> 498.6 M, configs[3] k_mlp2 16.4 -> 9.3 ms per
+// generation, 335 -> 363 M; the allocator's choice before was one wave with 48 AGPRs)
 #ifndef MV_MLP2_OCC_XML
-X
+#define MV_MLP2_OCC_XML 2
 #endif
 __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? MV_MLP2_OCC : MV_MLP2_OCC_XML)) void k_mlp2(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
