@@ -53,11 +53,12 @@ constexpr int SURV_T = MV_SURV_T;  // threads per survival workgroup (8 waves)
 #endif
 constexpr int SURV_T_BIG = MV_SURV_T_BIG;
 // threads of the N <= SURV_NLDS instance when the attack's states all fit two workgroups per
-// CU (SurvArgs.wide): 10 waves (round 5, headline: 225.4 vs 220.2 M evals/s with 512; 768:
-// 224.8 M; 896: 200.6 M; with 4,000 states (configs[2]) 768 threads lose occupancy: 461.5 vs
-// 481.4 M, so many states keep SURV_T)
+// CU (SurvArgs.wide): 9 waves (round 5, headline: 640 threads 225.4 vs 220.2 M evals/s with
+// 512; 576 / 704 against 640: 227.1 / 225.3 vs 226.3 M; 768: 224.8 M; 896: 200.6 M; with
+// 4,000 states (configs[2]) 768 threads lose occupancy: 461.5 vs 481.4 M, so many states
+// keep SURV_T)
 #ifndef MV_SURV_T_MID
-#define MV_SURV_T_MID 640
+#define MV_SURV_T_MID 576
 #endif
 constexpr int SURV_T_MID = MV_SURV_T_MID;
 constexpr int SURV_NMAX = 1024;  // merged individuals per state (n_pop 640: P + O = 963)
