@@ -474,6 +474,52 @@ def run_workload(name, w, args, device, world, rank, steps, warmup, bf16, crosso
     return result
 
 
+def time_generate(w, device, reps=2):
+    """The drop-in API end to end: Moeva2(...).generate(X, 1) on the workload's states, as
+    04_moeva.py:71-88 times it (metrics.time) -- host arrays in, the list of per-state result
+    objects out: bounds, state binding, the device attack, the final populations, their
+    non-dominated members (res.X / res.F) and the history copied to the host, result
+    objects.  Model / data loading (Moeva2's classifier, the engine's creation) happens in an
+    untimed first call, like the reference's load phase before its clock starts; the first
+    call's own wall is reported too (it also allocates the page-locked host buffers)."""
+    import torch
+
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, load_model
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+    from moeva2_amd.experiments.united.utils import get_constraints_from_str
+
+    c = get_constraints_from_str(w["project"])(os.path.join(RES, w["features"]),
+                                               os.path.join(RES, w["constraints"]))
+    X = load_states(w)
+    m = Moeva2(os.path.join(RES, w["model"]), c, ml_scaler=NpScaler(os.path.join(RES, w["scaler"])),
+               norm=w["norm"], n_gen=w["n_gen"], n_pop=w["n_pop"], n_offsprings=w["n_off"],
+               save_history=w["history"], seed=42, device=device)
+    m._classifier = Classifier(load_model(os.path.join(RES, w["model"])))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = m.generate(X, 1)
+    first = time.perf_counter() - t0
+    del res
+    walls = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = m.generate(X, 1)
+        walls.append(time.perf_counter() - t0)
+        n_front = sum(r.X.shape[0] for r in res)
+        del res
+    wall = min(walls)
+    P, O, G = w["n_pop"] + 3, w["n_off"], w["n_gen"]
+    evals = X.shape[0] * (P + (G - 1) * O)
+    del m
+    torch.cuda.empty_cache()
+    return {"call": "Moeva2(...).generate(X, 1) -> list of per-state results (host arrays in, "
+                    "pop / X / F / history on the host out)",
+            "states": int(X.shape[0]), "history": w["history"], "evals_per_s": evals / wall,
+            "wall_s": wall, "walls_s": walls, "first_call_wall_s": first,
+            "attack_wall_clock_per_1k_states_s": wall / X.shape[0] * 1000.0,
+            "front_members": int(n_front)}
+
+
 # The other BASELINE.json configs, one full-config attack each after the headline (N = 1):
 # (key, workload, classifier dtype, warm-up generations, profiled generations)
 EXTRA_CONFIGS = [
@@ -507,6 +553,8 @@ def main():
     ap.add_argument("--workload", default="rq1.botnet.static", choices=sorted(WORKLOADS))
     ap.add_argument("--n-gen", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-generate", action="store_true",
+                    help="skip the Moeva2.generate() end-to-end line (N = 1)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs' lines (N = 1 default: one full-config "
                          "attack each of configs[0], [2], [3], [4] after the headline)")
@@ -548,6 +596,13 @@ def main():
     result = run_workload(args.workload, w, args, device, world, rank, args.steps, args.warmup,
                           bf16, args.crossover)
     if rank == 0:
+        if world == 1 and not args.no_generate and not w["model"].startswith("synthetic:"):
+            torch.cuda.empty_cache()
+            g = time_generate(w, device)
+            g["vs_engine_step"] = g["wall_s"] / (result["ms_per_step"] * 1e-3)
+            result["generate"] = g
+            log(f"generate(): {g['evals_per_s'] / 1e6:.1f} M evals/s, wall {g['wall_s']:.3f} s "
+                f"({g['vs_engine_step']:.2f}x the engine step; first call {g['first_call_wall_s']:.3f} s)")
         if not args.no_cpu_baseline and world == 1 and not w["model"].startswith("synthetic:"):
             result["cpu_baseline"] = cpu_baseline(w, args.cpu_gens)
         # the other BASELINE configs (single GPU, default N = 1 run only): one timed

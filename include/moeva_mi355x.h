@@ -110,8 +110,9 @@ int mv_evaluate(mv_engine* e, int32_t n, const double* genes, double* F, double*
  * genes dev [B][n][V] -> x dev [B][n][D] with the bound states' x_init. */
 int mv_decode(mv_engine* e, int32_t n, const double* genes, double* x, void* stream);
 
-/* Entry points taking device buffers fail with MV_ERR_ARG when a buffer is device memory of
- * another GPU than the engine's (or objcalc's). */
+/* Every entry point taking device buffers fails with MV_ERR_ARG when a buffer is device
+ * memory of another GPU than the engine's (mlp's, objcalc's; for mv_survive and
+ * mv_select_parents, which take no engine: the current device's). */
 /* Constraints.evaluate (numpy path: values <= tol set to 0) on ML-space rows:
  * x dev [n][D] -> G dev [n][C].  Works on an engine created without a model. */
 int mv_constraints(mv_engine* e, int32_t n, const double* x, double* G, void* stream);
@@ -231,7 +232,19 @@ int mv_set_mlp_precision(mv_engine* e, int32_t bf16);
 int mv_get_attack_time(mv_engine* e, double* ms, int32_t* whole);
 /* Final population: genes dev [B][P][V], F dev [B][P][3] (either may be NULL). */
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream);
-/* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): dev buffer. */
+/* The final population's non-dominated members: the per-state result's X / F (moeva2.py:
+ * 167-171 returns pymoo's Result, whose X / F are the last population's first front).  The
+ * relation is pareto_operation.py:35-51's: i dominates j when F_i < F_j in some objective and
+ * F_i > F_j in none; a member is in the front when no member of its state's final population
+ * dominates it (the comparisons of a numpy any(<) / any(>) broadcast, so the mask is
+ * bit-identical to one computed on the host from mv_attack_population's F).  Outputs dev:
+ * front [B][P] uint8 (1 = member), offsets [B+1] int32 (state b's members are rows
+ * offsets[b] .. offsets[b+1]-1, population order), X [B*P][V] / Fx [B*P][3] (worst-case size;
+ * the first offsets[B] rows are written).  Any output may be NULL. */
+int mv_attack_front(mv_engine* e, uint8_t* front, int32_t* offsets, double* X, double* Fx,
+                    void* stream);
+/* History rows per state = P + (n_gen-1)*O, width 3 (reduced) or 3+C (full): hist [B][rows][w]
+ * a device buffer or page-locked host memory (hipHostMalloc / registered: one DMA). */
 int mv_attack_history(mv_engine* e, double* hist, void* stream);
 /* The attack's gene layout for the bound states (engine extension; no reference
  * counterpart).  mv_set_states finds the genes no attack on those states can change --
@@ -250,7 +263,9 @@ int mv_get_stored_genes(mv_engine* e, int32_t* stored, int32_t* n_stored);
  * reports after binding them. */
 int mv_gene_layout(mv_engine* e, int32_t B, const double* x_init, const double* xl,
                    const double* xu, int32_t* stored, int32_t* n_stored);
-/* Fix the layout of the following mv_set_states calls: stored [V] (1 = stored) as
+/* Fix the layout of the NEXT mv_set_states call (one call only; the request is consumed by
+ * it, refused or not, so a later binding on a shared engine derives its own): stored [V]
+ * (1 = stored) as
  * mv_gene_layout returned it for the WHOLE job, so a job split into batches or shards
  * (Moeva2.generate_sharded) runs every state in the same layout -- a state's f1 / f2
  * summation order, hence its trajectory, then does not depend on which states share its

@@ -155,6 +155,9 @@ struct mv_engine {
   double* ref = nullptr;
   std::vector<double> ref_host;  // the reference points currently in e->ref
   double* hist = nullptr;
+  // mv_attack_front scratch when the caller passes no mask / offsets (attack_allocs)
+  unsigned char* front_scr = nullptr;
+  int* off_scr = nullptr;
   bool attack_ready = false;
   bool has_model = false;
   long long* d_phase = nullptr;  // MV_SURV_PHASES=1: survival phase clocks [B][16]
@@ -636,11 +639,38 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
   for (int b = 0; b < B; ++b)
     if (minimize_class[b] < 0 || minimize_class[b] >= nout)
       return fail(MV_ERR_ARG, "minimize_class out of range");
+  // the attack's compact layout, when this state set has genes that never change (or the
+  // layout mv_set_gene_layout requested, checked against this batch before anything bound is
+  // released; the request applies to this call only)
+  std::vector<int> keep;
+  if (e->layout_req.empty()) {
+    keep = stored_genes(e, B, x_init, xl, xu);
+  } else {
+    const std::vector<int> req = std::move(e->layout_req);
+    e->layout_req.clear();
+    if (compact_allowed(e)) {
+      size_t j = 0;
+      for (int g = 0; g < e->hp.V; ++g) {
+        if (j < req.size() && req[j] == g) {
+          ++j;
+          continue;
+        }
+        for (int b = 0; b < B; ++b)
+          if (!gene_fixed(e->hp, g, x_init, xl, xu, b))
+            return fail(MV_ERR_ARG, "mv_set_gene_layout: gene " + std::to_string(g) +
+                                        " is not fixed in bound state " + std::to_string(b));
+      }
+      keep = req;
+      if ((int)keep.size() == e->hp.V) keep.clear();
+    }
+  }
   HIPCHK(hipDeviceSynchronize());
   e->free_list(e->cstate_allocs);
   e->free_list(e->state_allocs);
   e->free_list(e->attack_allocs);
   e->d_phase = nullptr;
+  e->front_scr = nullptr;
+  e->off_scr = nullptr;
   e->attack_ready = false;
   e->compact = false;
   e->B = 0;
@@ -657,26 +687,6 @@ int mv_set_states(mv_engine* e, int32_t B, const double* x_init, const double* x
                              (double*)e->s.gu, (unsigned char*)e->s.sblob, (float*)e->s.bias1,
                              e->genes0, (hipStream_t)stream));
   HIPCHK(release_rows(slot, (hipStream_t)stream));
-  // the attack's compact layout, when this state set has genes that never change (or the
-  // layout mv_set_gene_layout requested, checked against this batch)
-  std::vector<int> keep;
-  if (e->layout_req.empty()) {
-    keep = stored_genes(e, B, x_init, xl, xu);
-  } else if (compact_allowed(e)) {
-    size_t j = 0;
-    for (int g = 0; g < e->hp.V; ++g) {
-      if (j < e->layout_req.size() && e->layout_req[j] == g) {
-        ++j;
-        continue;
-      }
-      for (int b = 0; b < B; ++b)
-        if (!gene_fixed(e->hp, g, x_init, xl, xu, b))
-          return fail(MV_ERR_ARG, "mv_set_gene_layout: gene " + std::to_string(g) +
-                                      " is not fixed in bound state " + std::to_string(b));
-    }
-    keep = e->layout_req;
-    if ((int)keep.size() == e->hp.V) keep.clear();
-  }
   if (!keep.empty()) {
     if (keep != e->stored) {
       HIPCHK(hipDeviceSynchronize());
@@ -768,6 +778,8 @@ int mv_variation(mv_engine* e, int32_t P, int32_t O, uint64_t seed, int32_t gen,
   if (!e || P <= 1 || O <= 0 || (O & 1) || !pop || !parents || !off)
     return fail(MV_ERR_ARG, "bad mv_variation arguments (O must be even)");
   if (e->B <= 0) return fail(MV_ERR_STATE, "no states bound (mv_set_states)");
+  if (!on_device(pop, e->device) || !on_device(parents, e->device) || !on_device(off, e->device))
+    return fail(MV_ERR_ARG, "mv_variation: a buffer lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   RowsArgs a = base_rows(e);
   a.n = O;
@@ -798,6 +810,15 @@ int mv_survive(int32_t B, int32_t N, int32_t n_survive, const double* F, int32_t
     return fail(MV_ERR_ARG, "bad mv_survive arguments (N <= 1024, R <= 640, n_survive <= N)");
   if (surv_lds_bytes(N, R, 1) > 160 * 1024)
     return fail(MV_ERR_ARG, "mv_survive: N and R too large for the survival LDS workspace");
+  {  // no engine here: every buffer must live on the current device
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    const void* bufs[] = {F, ref_points, ideal, worst, extreme, has_extreme, survivors, rank,
+                          order, n_ranked, niche, dist, nadir};
+    for (const void* q : bufs)
+      if (!on_device(q, dev))
+        return fail(MV_ERR_ARG, "mv_survive: a buffer lives on another device than the current one");
+  }
   SurvArgs a{};
   a.N = N;
   a.n_survive = n_survive;
@@ -836,6 +857,12 @@ int mv_select_parents(int32_t B, int32_t P, int32_t O, uint64_t seed, int32_t ge
   while (p2 < slots) p2 <<= 1;
   if (P > 8192 || (size_t)p2 * 8 + (size_t)slots * 4 > 160 * 1024)
     return fail(MV_ERR_ARG, "mv_select_parents: population or offspring count too large");
+  {
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (!on_device(parents, dev))
+      return fail(MV_ERR_ARG, "mv_select_parents: parents live on another device than the current one");
+  }
   HIPCHK(launch_select(B, P, O, seed, 0u, gen, nullptr, parents, (hipStream_t)stream));
   return MV_OK;
 }
@@ -905,6 +932,8 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     };
     e->d_gphase = nullptr;
     e->gphase_n = 0;
+    e->front_scr = nullptr;
+    e->off_scr = nullptr;
     A(&e->pool, (size_t)B * S * V);
     A(&e->poolF, (size_t)B * S * 3);
     A(&e->pop_slot, (size_t)B * P);
@@ -1443,6 +1472,8 @@ void mv_mlp_destroy(mv_mlp* m) { delete m; }
 
 int mv_mlp_predict(mv_mlp* m, int32_t n, const double* x, double* proba, void* stream) {
   if (!m || n < 0 || (n > 0 && (!x || !proba))) return fail(MV_ERR_ARG, "bad mv_mlp_predict");
+  if (!on_device(x, m->device) || !on_device(proba, m->device))
+    return fail(MV_ERR_ARG, "mv_mlp_predict: a buffer lives on another device than the classifier");
   HIPCHK(hipSetDevice(m->device));
   MlpArgs a = m->a;
   a.n = n;
@@ -1598,6 +1629,9 @@ int mv_objcalc_score(mv_objcalc* o, int32_t B, int32_t n, const double* x_init, 
   if (total == 0) return MV_OK;
   if (!x_init || !x || !obj || !range_bad || !proba || (C > 0 && !G))
     return fail(MV_ERR_ARG, "null buffer");
+  if (!on_device(x_init, o->device) || !on_device(x, o->device) || !on_device(G, o->device) ||
+      !on_device(proba, o->device) || !on_device(obj, o->device) || !on_device(range_bad, o->device))
+    return fail(MV_ERR_ARG, "mv_objcalc_score: a buffer lives on another device than the calculator");
   HIPCHK(hipSetDevice(o->device));
   ObjArgs a{};
   a.total = total;
@@ -1644,6 +1678,8 @@ int mv_debug_survival_dump(double* out) {
 
 int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
   if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
+  if (!on_device(genes, e->device) || !on_device(F, e->device))
+    return fail(MV_ERR_ARG, "mv_attack_population: a buffer lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   // the pool's rows in the attack's layout -> genes of every one of the Vr genes
   const DProblem& ap = e->ap();
@@ -1660,6 +1696,31 @@ int mv_attack_population(mv_engine* e, double* genes, double* F, void* stream) {
                                     std::to_string(r[4]) + ", " + std::to_string(r[5]) +
                                     " failures)");
   }
+  return MV_OK;
+}
+
+int mv_attack_front(mv_engine* e, uint8_t* front, int32_t* offsets, double* X, double* Fx,
+                    void* stream) {
+  if (!e || !e->attack_ready) return fail(MV_ERR_STATE, "no attack has run");
+  if (!on_device(front, e->device) || !on_device(offsets, e->device) ||
+      !on_device(X, e->device) || !on_device(Fx, e->device))
+    return fail(MV_ERR_ARG, "mv_attack_front: a buffer lives on another device than the engine");
+  HIPCHK(hipSetDevice(e->device));
+  if (!front || !offsets) {  // scratch for the mask / offsets the caller does not want
+    if (!e->front_scr) {
+      hipError_t err = dalloc(&e->front_scr, (size_t)e->B * e->P);
+      if (err == hipSuccess) e->attack_allocs.push_back(e->front_scr);
+      if (err == hipSuccess) err = dalloc(&e->off_scr, (size_t)e->B + 1);
+      if (err == hipSuccess) e->attack_allocs.push_back(e->off_scr);
+      if (err != hipSuccess) return fail(MV_ERR_HIP, std::string("alloc: ") + hipGetErrorString(err));
+    }
+    if (!front) front = e->front_scr;
+    if (!offsets) offsets = e->off_scr;
+  }
+  const DProblem& ap = e->ap();
+  const int* cmap = ap.compact ? (const int*)(ap.vblob + vary_offsets(ap).cmap) : nullptr;
+  HIPCHK(launch_front(e->B, e->P, ap.V, ap.Vr, e->S, cmap, e->s.gl, e->pop_slot, e->pool,
+                      e->poolF, front, offsets, X, Fx, (hipStream_t)stream));
   return MV_OK;
 }
 
@@ -1704,9 +1765,11 @@ int mv_get_stored_genes(mv_engine* e, int32_t* stored, int32_t* n_stored) {
 int mv_attack_history(mv_engine* e, double* hist, void* stream) {
   if (!e || !e->attack_ready || !e->hist_mode) return fail(MV_ERR_STATE, "no history recorded");
   if (!hist) return fail(MV_ERR_ARG, "null hist");
+  if (!on_device(hist, e->device))
+    return fail(MV_ERR_ARG, "mv_attack_history: hist lives on another device than the engine");
   HIPCHK(hipSetDevice(e->device));
   HIPCHK(hipMemcpyAsync(hist, e->hist, (size_t)e->B * e->hist_rows * e->hist_w * sizeof(double),
-                        hipMemcpyDeviceToDevice, (hipStream_t)stream));
+                        hipMemcpyDefault, (hipStream_t)stream));
   return MV_OK;
 }
 

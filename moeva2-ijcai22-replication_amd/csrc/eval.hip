@@ -241,7 +241,7 @@ template <bool IDENT, int NT, bool SBX, bool PLAN = false, bool EARLY = false>
 __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row0, int rows_wg,
                                         unsigned char* smem) {
   static_assert(!EARLY || (IDENT && PLAN && !SBX), "early staging: k_genc two-point only");
-  constexpr bool FUSED = EARLY && MV_GENC_FUSED;  // the constraints inside the row loop
+  constexpr bool FUSED = EARLY;  // the constraints inside the row loop (genc_fused_lds)
   constexpr bool REGC = GEN_REGC && IDENT && NT <= 8;  // kernels.h gen_regc
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -250,8 +250,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const int V = p.V, Dm = p.Dm, Dm4 = p.Dm4;
   const bool ev = a.do_eval != 0;
   const VaryOff o = vary_offsets(p);
-  const GenLds L = FUSED ? genc_fused_lds(o, p) : EARLY ? genc_early_lds(o, p)
-                                                      : gen_lds(o, REGC, IDENT, ev);
+  const GenLds L = FUSED ? genc_fused_lds(o, p) : gen_lds(o, REGC, IDENT, ev);
   const unsigned char* sblob = a.s.sblob + (size_t)b * o.sb;
   // the rows' matings and destinations first: their round trips (the parents come from the
   // previous k_survive) overlap the LDS staging instead of following it
@@ -397,8 +396,9 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   // round trip is ~4 us, several rows' worth of work, and one row of prefetch left each row
   // waiting on its loads (r03 phase clocks: ~9.6 k cycles per row).  The first two rows'
   // loads go out before the mutation draws, whose gathers and pow chains then overlap them.
-  // MV_GENC_PF = 1: one row in flight instead of two (k_genc's register budget, A/B)
-  constexpr bool PF2 = !(EARLY && MV_GENC_PF == 1);
+  // k_genc's fused instance keeps one row in flight (its register budget; round 5: 220.6 vs
+  // 219.3 M evals/s with two, k_genc 87.3 vs 89.3 us, no spilled registers)
+  constexpr bool PF2 = !EARLY;
   double xa[NT], xb[PF2 ? NT : 1];
   auto preload = [&]() {
     if (nrw > 0) load_row(0, xa);
@@ -596,13 +596,10 @@ __global__ __launch_bounds__(VARY_T) void k_gen(int slot, int gen, int hist_row0
 // evaluates its (register-packed) ops.
 // SLIM (k_genc, DProblem.slim): region S staged instead of region A, the lane ops' packed
 // words loaded straight from the problem blob (see kernels.h).
-// STAGED (k_genc's early-staged instance): regions S and X are already in LDS, behind the
-// k_genc phase barrier.
-template <bool FULL, bool IDENT, int NT, bool SLIM = false, bool STAGED = false>
+template <bool FULL, bool IDENT, int NT, bool SLIM = false>
 __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int rows_wg,
                                           unsigned char* smem, bool have_dst = false,
                                           int dst_pre = 0) {
-  static_assert(!STAGED || SLIM, "early staging: the slim program only");
   const DProblem& p = a.p;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const RowChunk rc = row_chunk<CONS_W>(a.n, rows_wg, wave);
@@ -650,11 +647,11 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
       const unsigned w = gw[c < n_lane ? c : 0];
       opw[k] = (k < kops && c < n_lane) ? w : 0u;
     }
-    if (!STAGED) glds_copy<CONS_T>(smem, p.vblob + o.s_at, pa, wave, lane);
+    glds_copy<CONS_T>(smem, p.vblob + o.s_at, pa, wave, lane);
   } else {
     glds_copy<CONS_T>(smem, p.vblob, pa, wave, lane);
   }
-  if (!STAGED) glds_copy<CONS_T>(smem + pa, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
+  glds_copy<CONS_T>(smem + pa, a.s.sblob + (size_t)b * o.sb, o.x_end, wave, lane);
   int ginf[NT];
   {
     const int* gi = (const int*)(p.vblob + o.ginfo);
@@ -665,10 +662,8 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
       ginf[t] = g < V ? w : 0;
     }
   }
-  if (!STAGED) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
   if (MV_CLOCKS && a.gphase && tid == 0) a.gphase[(size_t)blockIdx.x * 8 + 4] = clock64();
   double* xrow = (double*)(smem + pa + o.x_end + wave * (SLIM ? o.rbs : o.rb));
   const double* s_xi = (const double*)(smem + pa + o.xi);
@@ -794,16 +789,16 @@ __global__ MV_GENC_BOUNDS void k_genc(int slot, int gen, int hist_row0, int rows
     a.gphase[(size_t)blockIdx.x * 8 + 0] = clock64();
     a.gphase[(size_t)blockIdx.x * 8 + 6] = wall_clock64();
   }
-  constexpr bool EARLY = SLIM && !SBX;  // the whole LDS staged at the start (genc_early_lds)
+  constexpr bool EARLY = SLIM && !SBX;  // the whole LDS staged at the start (genc_fused_lds)
   const int orow_v = gen_rows<IDENT, NT, SBX, true, EARLY>(a, gen, hist_row0, rows_wg, smem);
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) a.gphase[(size_t)blockIdx.x * 8 + 3] = clock64();
   // every child store has completed (vmcnt 0) before the barrier, so phase 2's loads of the
   // same rows see them; the phase-1 LDS images are dead and phase 2 stages over them.  Both
   // phases chunk the rows alike (VARY_T == CONS_T), so a lane's destination row is its own.
-  if (!(EARLY && MV_GENC_FUSED)) {  // FUSED: the constraints ran inside phase 1's row loop
+  if constexpr (!EARLY) {  // EARLY: the constraints ran inside phase 1's row loop
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    cons_rows<false, IDENT, NT, SLIM, EARLY>(a, hist_row0, rows_wg, smem, true, orow_v);
+    cons_rows<false, IDENT, NT, SLIM>(a, hist_row0, rows_wg, smem, true, orow_v);
   }
   if (MV_CLOCKS && a.gphase && threadIdx.x == 0) {
     a.gphase[(size_t)blockIdx.x * 8 + 5] = clock64();
@@ -2070,10 +2065,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     const bool slim = a.p.slim != 0;
     const size_t lc = slim ? cons_lds_slim(o) : cons_lds_total(o);
     static const size_t pad = lds_pad("MV_LDS_PAD_GENC");
-    const size_t lds = (slim && !sbx ? (MV_GENC_FUSED ? genc_fused_lds(o, a.p).total
-                                                      : genc_early_lds(o, a.p).total)
-                                     : (lg > lc ? lg : lc)) +
-                       pad;
+    const size_t lds = (slim && !sbx ? genc_fused_lds(o, a.p).total : (lg > lc ? lg : lc)) + pad;
     // k_genc takes mode 1's draws from the variation plan (mv_attack_run's k_survive)
     if (a.mode == 1 && !(a.plan_hdr && a.plan_mw && a.plan_mu)) return hipErrorInvalidValue;
     if (nt == 4) return genc_go<4>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);

@@ -130,36 +130,11 @@ __host__ __device__ inline GenLds gen_lds(const VaryOff& o, bool regc, bool iden
   l.total = at;
   return l;
 }
-// k_genc's two-point slim instance stages everything at its start: phase 2's region S and X
-// at 0, and phase 1's region E (and C unless xml_direct) in the space of phase 2's row
-// buffers, which are written only after the phase barrier (so no staging sits between the
-// phases).  Phase 1 reads its gene tables from the problem blob (the variation plan leaves
-// only the gene info there).
-__host__ __device__ inline GenLds genc_early_lds(const VaryOff& o, const DProblem& p) {
-  GenLds l{};
-  const unsigned rows_at = (o.s_end - o.s_at) + o.x_end;
-  const unsigned e_sz = o.sb - o.e_at;
-  l.b_at = 0;
-  l.e_at = rows_at;
-  l.c_at = rows_at + e_sz;
-  l.x_at = o.s_end - o.s_at;
-  l.rows_at = rows_at;
-  const unsigned ph1 = e_sz + (p.xml_direct ? 0u : (o.c_end - o.c_at));
-  const unsigned ph2 = CONS_W * o.rbs;
-  l.total = rows_at + (ph1 > ph2 ? ph1 : ph2);
-  return l;
-}
-// MV_GENC_FUSED (k_genc's two-point slim instance): the constraint program runs inside
-// phase 1's row loop on the child genes still in registers -- no second row loop, no
-// re-read of the children, no phase barrier.  LDS: [S][X][E (and C)][one row per wave].
-#ifndef MV_GENC_FUSED
-#define MV_GENC_FUSED 1
-#endif
-// MV_GENC_PF: parent rows in flight ahead of the row k_genc's fused instance finishes: 1
-// (round 5: 220.6 vs 219.3 M evals/s with 2, k_genc 87.3 vs 89.3 us, no spilled registers)
-#ifndef MV_GENC_PF
-#define MV_GENC_PF 1
-#endif
+// k_genc's two-point slim instance (EARLY): everything is staged at its start and the
+// constraint program runs inside phase 1's row loop on the child genes still in registers --
+// no second row loop, no re-read of the children, no phase barrier (round 5: k_genc PMC
+// 343 -> 250 MB per launch).  Phase 1 reads its gene tables from the problem blob (the
+// variation plan leaves only the gene info there).  LDS: [S][X][E (and C)][one row per wave].
 __host__ __device__ inline GenLds genc_fused_lds(const VaryOff& o, const DProblem& p) {
   GenLds l{};
   const unsigned ssz = o.s_end - o.s_at;
@@ -246,5 +221,11 @@ hipError_t launch_objectives(const ObjArgs& a, hipStream_t stream);
 hipError_t launch_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap,
                              const double* glr, const int* pop_slot, const double* pool,
                              const double* poolF, double* genes, double* F, hipStream_t stream);
+// final population -> non-dominated mask front [B][P], row offsets [B+1], and (optional) the
+// members' genes X [rows][Vr] / objectives Fx [rows][3] packed in state and population order
+hipError_t launch_front(int B, int P, int V, int Vr, int S, const int* cmap, const double* glr,
+                        const int* pop_slot, const double* pool, const double* poolF,
+                        unsigned char* front, int* offsets, double* X, double* Fx,
+                        hipStream_t stream);
 
 }  // namespace mv

@@ -486,13 +486,8 @@ __device__ __forceinline__ void softmax_all(const double (&z)[8], int nout, doub
 template <int T = VARY_T>
 __device__ __forceinline__ void glds_copy(unsigned char* lds, const unsigned char* g,
                                           unsigned nbytes, int wave, int lane) {
-#ifdef MV_NO_LDS_DMA
-  for (unsigned off = wave * 1024u; off < nbytes; off += T * 16u)
-    *(uint4*)(lds + off + lane * 16) = *(const uint4*)(g + off + lane * 16);
-#else
   for (unsigned off = wave * 1024u; off < nbytes; off += T * 16u)
     __builtin_amdgcn_global_load_lds(g + off + lane * 16, lds + off, 16, 0, 0);
-#endif
 }
 
 // Rows of one k_gen / k_cons workgroup: a chunk of one state's rows; wave w takes rows

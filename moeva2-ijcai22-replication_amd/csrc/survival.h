@@ -33,11 +33,6 @@ static __device__ double g_surv_dump[SURV_DUMP_N];
 namespace mv {
 
 constexpr int SURV_TMAX = 1024;
-// MV_ASSOC_F64: the association pre-filter in fp64 (directions as double4 in LDS) instead of
-// fp32 with crowded-direction refinement
-#ifndef MV_ASSOC_F64
-#define MV_ASSOC_F64 1
-#endif
 // its first sweep's unroll (2: 104 VGPRs, two survival workgroups per CU; 1: 80, three)
 #ifndef MV_ASSOC_UNROLL
 #define MV_ASSOC_UNROLL 1
@@ -47,7 +42,7 @@ struct SurvLds {
   double* F;        // [N*3]
   const double* ref;  // global: the reference points (read-only, L2-resident)      // [R*3]
   double* U;        // [(R+3)*3] normalised reference directions
-  float4* Uf;       // [R+3] the same in fp32 (association pre-filter)
+  double4* Uf;      // [R+3] the same as double4 (association pre-filter)
   double* dist;     // [N]
   double* red;      // [waves*16] reduction scratch
   double* scal;     // [40] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9) prev ext(9)
@@ -144,7 +139,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(F, (size_t)NW * 64 * 3 * 8)  // rows past N hold NaN (dominance padding)
   o.ref = 0;                        // unused: a.ref in global memory
   TAKE(U, (size_t)RN * 3 * 8)
-  TAKE(Uf, (size_t)RN * (MV_ASSOC_F64 ? 32 : 16))
+  TAKE(Uf, (size_t)RN * 32)  // unit directions as double4 (association pre-filter)
   TAKE(dist, (size_t)N * 8)
   TAKE(red, ((threads ? threads : surv_threads(N)) / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
@@ -487,7 +482,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   L.F = (double*)(smem + o.F);
   L.ref = a.ref;  // global (surv_offsets)
   L.U = (double*)(smem + o.U);
-  L.Uf = (float4*)(smem + o.Uf);
+  L.Uf = (double4*)(smem + o.Uf);
   L.dist = (double*)(smem + o.dist);
   L.red = (double*)(smem + o.red);
   L.scal = (double*)(smem + o.scal);
@@ -948,11 +943,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
       const double nrm = sqrt((res[0] * res[0] + res[1] * res[1]) + res[2] * res[2]);
       for (int k = 0; k < 3; ++k) L.U[r * 3 + k] = res[k] / nrm;
-#if MV_ASSOC_F64
-      ((double4*)L.Uf)[r] = make_double4(L.U[r * 3], L.U[r * 3 + 1], L.U[r * 3 + 2], 0.0);
-#else
-      L.Uf[r] = make_float4((float)L.U[r * 3], (float)L.U[r * 3 + 1], (float)L.U[r * 3 + 2], 0.f);
-#endif
+      L.Uf[r] = make_double4(L.U[r * 3], L.U[r * 3 + 1], L.U[r * 3 + 2], 0.0);
     }
     if (tid == 0) L.iscal[15] = 0;
     __syncthreads();
@@ -973,7 +964,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     // the sequential scan).
     const int nh = RN >> 1;  // directions per half (wave-uniform loop counts); an odd RN's
                              // last direction goes to the second half's chain 0
-#if MV_ASSOC_F64
     for (int v = tid; v < 2 * n_ranked; v += T) {
       const int p = v >> 1, hf = v & 1;
       const int jb = hf ? nh : 0;
@@ -999,7 +989,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       // (late botnet generations), so no refinement sweeps are needed; more than four hits
       // (near-duplicate directions) or a NaN / overflow go to the exact pass below.
       const double nn = fma(Nn[0], Nn[0], fma(Nn[1], Nn[1], Nn[2] * Nn[2]));
-      const double4* Ud = (const double4*)L.Uf;
+      const double4* Ud = L.Uf;
       auto d2f = [&](int j) {
         const double4 u = Ud[j];
         const double sp = fma(Nn[0], u.x, fma(Nn[1], u.y, Nn[2] * u.z));
@@ -1093,174 +1083,6 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         L.key[atomicAdd(&L.iscal[15], 1)] = p;
       }
     }
-#else
-    for (int v = tid; v < 2 * n_ranked; v += T) {
-      const int p = v >> 1, hf = v & 1;
-      const int jb = hf ? nh : 0;
-      const bool odd = hf && (RN & 1);
-      const int m = L.I[p];
-      double Nn[3];
-      for (int k = 0; k < 3; ++k) Nn[k] = (L.F[m * 3 + k] - ideal[k]) / den[k];
-      // fp32 pre-filter of the squared perpendicular distances, as |N|^2 - (N.u)^2 for the
-      // unit directions u (3 FMAs + 1 per direction).  Its error is below 2e-6 |N|^2
-      // (dot product 3.1e-7 |N|, rounding of u to fp32 1.2e-7, |N|^2 1.8e-7, all relative),
-      // so only directions whose fp32 value is within tol = 3e-5 (|N|^2 + best) of the fp32
-      // minimum can hold the fp64 minimum: those few get the exact fp64 distance and
-      // np.argmin's order (first index among equal sqrt'ed distances).  A NaN or overflow
-      // sends the individual to the full exact pass below.
-      // The pre-filter runs on N scaled by a power of two (exact) to a largest component in
-      // [1, 2): argmin of the perpendicular distance is scale-invariant, and unscaled
-      // coordinates overflow / underflow fp32 whenever nadir - ideal collapses in one
-      // objective (den = 1e-12): at botnet generation 1000 that sent 72 of 303 individuals
-      // per state to the serial exact pass below.  The candidates are then evaluated exactly
-      // on the unscaled N.
-      const double amax = fmax(fabs(Nn[0]), fmax(fabs(Nn[1]), fabs(Nn[2])));
-      const double sc = amax > 0.0 && amax < __builtin_inf() ? ldexp(1.0, -ilogb(amax)) : 1.0;
-      const float n0 = (float)(Nn[0] * sc), n1 = (float)(Nn[1] * sc), n2 = (float)(Nn[2] * sc);
-      const float nn = fmaf(n0, n0, fmaf(n1, n1, n2 * n2));
-      auto d2f = [&](int j) {
-        const float4 u = L.Uf[j];
-        const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
-        return fmaf(-sp, sp, nn);
-      };
-      if (Nn[0] == 0.0 && Nn[1] == 0.0 && Nn[2] == 0.0 && !signbit(Nn[0]) && !signbit(Nn[1]) &&
-          !signbit(Nn[2])) {  // at the ideal point: every distance is exactly +0 (both lanes)
-        if (!hf) {
-          L.niche[p] = 0;
-          L.dist[p] = 0.0;
-        }
-        continue;
-      }
-      // 4 independent min chains over the half's directions jb + 4k + u (chain 0 also takes
-      // the tail); v_min_f32 directly (fminf would re-canonicalise the chain every step).
-      // With |N|^2 finite every d is finite (|u| = 1); otherwise the chains stay +inf and
-      // the individual takes the exact pass below.
-      float b0 = __builtin_inff(), b1 = b0, b2 = b0, b3 = b0;
-      const int n4 = nh >> 2;
-      if (nn < __builtin_inff()) {
-#pragma unroll 2
-        for (int k = 0; k < n4; ++k) {
-          const int j = jb + 4 * k;
-          b0 = vmin_f32(b0, d2f(j));
-          b1 = vmin_f32(b1, d2f(j + 1));
-          b2 = vmin_f32(b2, d2f(j + 2));
-          b3 = vmin_f32(b3, d2f(j + 3));
-        }
-        for (int j = jb + 4 * n4; j < jb + nh; ++j) b0 = vmin_f32(b0, d2f(j));
-        if (odd) b0 = vmin_f32(b0, d2f(RN - 1));
-      }
-      float best = fminf(fminf(b0, b1), fminf(b2, b3));
-      best = fminf(best, __shfl_xor(best, 1, 64));
-      const float lim = best + 3e-5f * (nn + best);
-      if (lim < __builtin_inff()) {  // false on NaN / inf (the same in both lanes)
-        double bd = __builtin_inf();
-        int bj = 0;
-        auto cand = [&](int j) {  // exact fp64 distance, np.argmin order
-          const double* u = &L.U[j * 3];
-          const double s = (Nn[0] * u[0] + Nn[1] * u[1]) + Nn[2] * u[2];
-          const double e0 = s * u[0] - Nn[0], e1 = s * u[1] - Nn[1], e2 = s * u[2] - Nn[2];
-          const double dd = sqrt((e0 * e0 + e1 * e1) + e2 * e2);
-          if (arg_better(dd, j, bd, bj)) {
-            bd = dd;
-            bj = j;
-          }
-        };
-        // second sweep only over the chains whose minimum is within lim (usually just the
-        // chain holding the minimum).  d2f is the same expression as in the first sweep, so
-        // no candidate is missed, and arg_better is a total order, so the visiting order
-        // does not change the result.
-        const unsigned cm0 = (b0 <= lim ? 1u : 0u) | (b1 <= lim ? 2u : 0u) |
-                             (b2 <= lim ? 4u : 0u) | (b3 <= lim ? 8u : 0u);
-        // collect the candidate indices first (cheap selects, so the lanes' hits at
-        // different steps cost little), then evaluate them in a wave-uniform loop: calling
-        // the fp64 distance inside the sweep ran it once per step at which ANY lane had a hit
-        int c0 = 0, c1 = 0, c2 = 0, c3 = 0, nc = 0;
-        auto hit = [&](int jc) {
-          c0 = nc == 0 ? jc : c0;
-          c1 = nc == 1 ? jc : c1;
-          c2 = nc == 2 ? jc : c2;
-          c3 = nc == 3 ? jc : c3;
-          ++nc;
-        };
-        // every direction of this half whose fp32 value is within lim, in chain order
-        auto sweep = [&](auto&& on_hit) {
-          unsigned cm = cm0;
-          while (cm) {
-            const int u = __builtin_ctz(cm);
-            cm &= cm - 1u;
-            int k = 0;
-            for (; k + 4 <= n4; k += 4) {  // four independent LDS reads in flight
-              const int jc = jb + 4 * k + u;
-              const float d0 = d2f(jc), d1 = d2f(jc + 4), d2 = d2f(jc + 8), d3 = d2f(jc + 12);
-              if (d0 <= lim) on_hit(jc);
-              if (d1 <= lim) on_hit(jc + 4);
-              if (d2 <= lim) on_hit(jc + 8);
-              if (d3 <= lim) on_hit(jc + 12);
-            }
-            for (; k < n4; ++k) {
-              const int jc = jb + 4 * k + u;
-              if (d2f(jc) <= lim) on_hit(jc);
-            }
-            if (u == 0) {
-              for (int jc = jb + 4 * n4; jc < jb + nh; ++jc)
-                if (d2f(jc) <= lim) on_hit(jc);
-              if (odd && d2f(RN - 1) <= lim) on_hit(RN - 1);
-            }
-          }
-        };
-        sweep(hit);
-        bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;
-        if (ovf) {
-          // Crowded directions (late botnet generations: nadir - ideal of f2 shrinks to ~0.017,
-          // the aspiration directions bunch up near the f2 axis and 20+ of them pass lim):
-          // refine the hits with the perpendicular vector itself, e = (n.u) u - n in fp32,
-          // which has no |n|^2 - s^2 cancellation.  Its error against the exact distance is
-          // below 8.4e-7 |n||e| + 3e-7 |e|^2 + 2e-13 |n|^2 (s: 3e-7 |n|; e: 4.2e-7 |n| +
-          // 6e-8 |e|; |e|^2: 3 roundings), so every hit within twice that (taken 2.4x
-          // larger) of the refined minimum rb -- the fp64 argmin among them -- is kept.  Both
-          // halves of the pair take the branch (ovf is symmetric), so the shuffles are safe.
-          auto d2d = [&](int j) {
-            const float4 u = L.Uf[j];
-            const float sp = fmaf(n0, u.x, fmaf(n1, u.y, n2 * u.z));
-            const float e0 = fmaf(sp, u.x, -n0), e1 = fmaf(sp, u.y, -n1);
-            const float e2 = fmaf(sp, u.z, -n2);
-            return fmaf(e0, e0, fmaf(e1, e1, e2 * e2));
-          };
-          float rb = __builtin_inff();
-          sweep([&](int jc) { rb = fminf(rb, d2d(jc)); });
-          rb = fminf(rb, __shfl_xor(rb, 1, 64));
-          const float lr = rb + (4e-6f * sqrtf(nn) * sqrtf(rb) + 2e-6f * rb + 1e-11f * nn);
-          nc = 0;
-          sweep([&](int jc) {
-            if (d2d(jc) <= lr) hit(jc);
-          });
-          ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;  // rare: the full exact pass below
-        }
-        if (!ovf) {
-          if (nc > 0) cand(c0);
-          if (nc > 1) cand(c1);
-          if (nc > 2) cand(c2);
-          if (nc > 3) cand(c3);
-        }
-        const double od = __shfl_xor(bd, 1, 64);
-        const int oj = __shfl_xor(bj, 1, 64);
-        if (arg_better(od, oj, bd, bj)) {
-          bd = od;
-          bj = oj;
-        }
-        if (!hf) {
-          if (ovf) {
-            L.key[atomicAdd(&L.iscal[15], 1)] = p;
-          } else {
-            L.niche[p] = bj;
-            L.dist[p] = bd;
-          }
-        }
-      } else if (!hf) {
-        L.key[atomicAdd(&L.iscal[15], 1)] = p;
-      }
-    }
-#endif
     __syncthreads();
     PHASE(10)
     // exact np.argmin over sqrt'ed distances for the flagged individuals: one individual per

@@ -66,6 +66,110 @@ __global__ void k_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap
   }
 }
 
+// Final population -> its non-dominated members (the per-state result's X / F, pymoo's
+// `opt` of the last generation).  Relation of pareto_operation.py:35-51: i dominates j when
+// F_i < F_j in some objective and F_i > F_j in none; a member is in the front when no other
+// member dominates it (identical rows do not dominate each other).  One workgroup per state,
+// the state's F in LDS (structure of arrays), one member per thread: P <= 1022 compares
+// against broadcast LDS reads.  offsets[b + 1] receives the state's front size.
+__global__ __launch_bounds__(256) void k_front_mask(int P, int S, const int* pop_slot,
+                                                     const double* poolF, unsigned char* front,
+                                                     int* offsets) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* fs = (double*)smem;  // [3][P]
+  __shared__ int n_front;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) n_front = 0;
+  for (int j = threadIdx.x; j < P; j += blockDim.x) {
+    const int s = MV_IDX(pop_slot[(size_t)b * P + j], S, CK_SURV_SLOT);
+    const double* f = poolF + ((size_t)b * S + s) * 3;
+    fs[j] = f[0];
+    fs[P + j] = f[1];
+    fs[2 * P + j] = f[2];
+  }
+  __syncthreads();
+  int mine = 0;
+  for (int j = threadIdx.x; j < P; j += blockDim.x) {
+    const double a0 = fs[j], a1 = fs[P + j], a2 = fs[2 * P + j];
+    bool dom = false;
+    for (int i = 0; i < P && !dom; ++i) {
+      const double c0 = fs[i], c1 = fs[P + i], c2 = fs[2 * P + i];
+      const bool less = c0 < a0 || c1 < a1 || c2 < a2;
+      const bool more = c0 > a0 || c1 > a1 || c2 > a2;
+      dom = less && !more;
+    }
+    front[(size_t)b * P + j] = dom ? 0 : 1;
+    mine += dom ? 0 : 1;
+  }
+  if (mine) atomicAdd(&n_front, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) offsets[b + 1] = n_front;
+}
+
+// offsets[1..B] (front sizes) -> exclusive row offsets [0..B] (in place), one workgroup:
+// each thread sums a contiguous run, a block scan of the run sums, then the runs rewritten.
+__global__ __launch_bounds__(1024) void k_front_scan(int B, int* offsets) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, T = blockDim.x;
+  const int per = (B + T - 1) / T, lo = t * per, hi = min(B, lo + per);
+  int sum = 0;
+  for (int b = lo; b < hi; ++b) sum += offsets[b + 1];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < T; d <<= 1) {
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;  // exclusive prefix of this thread's run
+  for (int b = lo; b < hi; ++b) {
+    const int c = offsets[b + 1];
+    offsets[b + 1] = run + c;
+    run += c;
+  }
+  if (t == 0) offsets[0] = 0;
+}
+
+// Front members -> X rows offsets[b] .. offsets[b + 1] - 1 (population order), genes of every
+// one of the Vr genes (as k_gather_pop) and their F.
+__global__ __launch_bounds__(256) void k_front_gather(int P, int V, int Vr, int S, const int* cmap,
+                                                       const double* glr, const int* pop_slot,
+                                                       const double* pool, const double* poolF,
+                                                       const unsigned char* front,
+                                                       const int* offsets, double* X, double* Fx) {
+  __shared__ int rank[1024];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  if (wave == 0) {
+    int base = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int c = 0; c < P; c += 64) {
+      const int j = c + lane;
+      const bool in = j < P && front[(size_t)b * P + j];
+      const unsigned long long m = __ballot(in);
+      if (j < P) rank[j] = in ? base + __popcll(m & below) : -1;
+      base += __popcll(m);
+    }
+  }
+  __syncthreads();
+  const size_t row0 = (size_t)offsets[b];
+  for (int j = wave; j < P; j += nw) {
+    const int r = rank[j];
+    if (r < 0) continue;
+    const int s = MV_IDX(pop_slot[(size_t)b * P + j], S, CK_SURV_SLOT);
+    const double* src = pool + ((size_t)b * S + s) * V;
+    if (X) {
+      double* dst = X + (row0 + r) * Vr;
+      for (int g = lane; g < Vr; g += 64) {
+        const int c = cmap ? cmap[g] : g;
+        dst[g] = c >= 0 ? src[c] : glr[(size_t)b * Vr + g];
+      }
+    }
+    if (Fx && lane < 3) Fx[(row0 + r) * 3 + lane] = poolF[((size_t)b * S + s) * 3 + lane];
+  }
+}
+
 MV_DEFINE_TAKE_CHECKS(take_checks_survive)
 
 hipError_t take_survival_dump(double* out) {
@@ -144,6 +248,21 @@ hipError_t launch_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap
                              const double* poolF, double* genes, double* F, hipStream_t stream) {
   hipLaunchKernelGGL(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, Vr, S, cmap, glr,
                      pop_slot, pool, poolF, genes, F);
+  return hipGetLastError();
+}
+
+hipError_t launch_front(int B, int P, int V, int Vr, int S, const int* cmap, const double* glr,
+                        const int* pop_slot, const double* pool, const double* poolF,
+                        unsigned char* front, int* offsets, double* X, double* Fx,
+                        hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (P < 1 || P > 1024 || !front || !offsets) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_front_mask, dim3(B), dim3(256), (size_t)P * 3 * sizeof(double), stream, P,
+                     S, pop_slot, poolF, front, offsets);
+  hipLaunchKernelGGL(k_front_scan, dim3(1), dim3(1024), 0, stream, B, offsets);
+  if (X || Fx)
+    hipLaunchKernelGGL(k_front_gather, dim3(B), dim3(256), 0, stream, P, V, Vr, S, cmap, glr,
+                       pop_slot, pool, poolF, front, offsets, X, Fx);
   return hipGetLastError();
 }
 

@@ -23,7 +23,8 @@ OP = dict(DIFF=1, RATIO_SAFE=2, ABS_SUMDIFF=3, LCLD_INSTALL=4, LCLD_TERM=5, ABS_
 EXPORTED = [
     "mv_last_error", "mv_device_count", "mv_engine_create", "mv_engine_destroy",
     "mv_set_states", "mv_evaluate", "mv_decode", "mv_constraints", "mv_survive", "mv_select_parents",
-    "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_history",
+    "mv_variation", "mv_attack_run", "mv_attack_population", "mv_attack_front",
+    "mv_attack_history",
     "mv_set_profiling", "mv_get_kernel_times", "mv_get_phase_times", "mv_get_row_kernel",
     "mv_get_mlp_kernel", "mv_set_attack_mode",
     "mv_set_crossover", "mv_set_mlp_precision",
@@ -98,6 +99,7 @@ def lib():
             "mv_variation": [vp, C.c_int32, C.c_int32, C.c_uint64, C.c_int32, vp, vp, vp, vp],
             "mv_attack_run": [vp, C.POINTER(AttackParams), vp],
             "mv_attack_population": [vp, vp, vp, vp],
+            "mv_attack_front": [vp, vp, vp, vp, vp, vp],
             "mv_attack_history": [vp, vp, vp],
             "mv_set_profiling": [vp, C.c_int32],
             "mv_get_kernel_times": [vp, _f64p, _f64p, _f64p, _i32p],
@@ -339,8 +341,24 @@ class Engine:
     def attack_population(self, genes=None, F=None, stream=None):
         check(lib().mv_attack_population(self._h, _ptr(genes), _ptr(F), _stream(stream)))
 
-    def attack_history(self, hist, stream=None):
-        check(lib().mv_attack_history(self._h, _ptr(hist), _stream(stream)))
+    def attack_front(self, front=None, offsets=None, X=None, Fx=None, stream=None):
+        """The final population's non-dominated members (mv_attack_front): front (B, P)
+        uint8, offsets (B + 1,) int32 and the members' genes X (B * P, V) / objectives
+        Fx (B * P, 3) packed by state in population order (first offsets[B] rows)."""
+        check(lib().mv_attack_front(self._h, _ptr(front), _ptr(offsets), _ptr(X), _ptr(Fx),
+                                    _stream(stream)))
+
+    def attack_history(self, hist, stream=None, host=False):
+        """History rows (B, P + (n_gen - 1) O, 3 | 3 + C) into a device tensor, or with
+        host=True a contiguous host tensor -- page-locked (pinned / hipHostRegister'ed) for a
+        direct DMA; mv_attack_history copies with hipMemcpyDefault."""
+        if host:
+            if hist.is_cuda or not hist.is_contiguous():
+                raise ValueError("attack_history(host=True): a contiguous host tensor")
+            p = C.c_void_p(hist.data_ptr())
+        else:
+            p = _ptr(hist)
+        check(lib().mv_attack_history(self._h, p, _stream(stream)))
 
     def set_profiling(self, on: bool):
         check(lib().mv_set_profiling(self._h, int(on)))

@@ -170,6 +170,32 @@ class TabularConstraints(Constraints):
                 f"{dynamic_number} feature min and max are dynamic but no input were provided.")
         return feature_min, feature_max
 
+    def feature_min_max_batch(self, X: np.ndarray):
+        """``get_feature_min_max(dynamic_input=x)`` for every row x of X at once (engine
+        extension, Moeva2.generate's per-state bounds): (xl, xu), each (n, D) fp64, the
+        same values as the per-row calls -- the static bounds are converted once exactly as
+        lcld_constraints.py:248-249 converts them, the dynamic ones are X's own values."""
+        X = np.asarray(X, dtype=np.float64)
+        st = getattr(self, "_static_bounds", None)
+        if st is None:
+            st = self._static_bounds = self._static_min_max() + self._dynamic_masks()
+        lo, hi, min_dyn, max_dyn = st
+        return np.where(min_dyn, X, lo), np.where(max_dyn, X, hi)
+
+    def _dynamic_masks(self):
+        return (self._feature_min.astype(str) == "dynamic",
+                self._feature_max.astype(str) == "dynamic")
+
+    def _static_min_max(self):
+        """The non-dynamic entries of get_feature_min_max, converted as it converts them
+        (dynamic entries left at 0.0)."""
+        min_dyn, max_dyn = self._dynamic_masks()
+        feature_min = np.array([0.0] * self._feature_min.shape[0])
+        feature_max = np.array([0.0] * self._feature_max.shape[0])
+        feature_min[~min_dyn] = self._feature_min[~min_dyn]
+        feature_max[~max_dyn] = self._feature_max[~max_dyn]
+        return feature_min, feature_max
+
     # -- device evaluation
     def _constraint_engine(self, device=None):
         """The constraint-only engine on ``device`` (default: torch's current device), built

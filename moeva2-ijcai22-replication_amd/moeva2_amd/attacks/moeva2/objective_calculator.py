@@ -21,7 +21,7 @@ import numpy as np
 from .classifier import Classifier
 from .constraints import Constraints
 from .feature_encoder import get_encoder_from_constraints
-from .utils import get_ohe_masks
+from .utils import _pop_x, get_ohe_masks
 
 
 class ObjectiveCalculator:
@@ -200,8 +200,7 @@ class ObjectiveCalculator:
 
     def _pops_ml(self, results):
         initial_states = [result.initial_state for result in results]
-        pops_x = [np.array([ind.X.astype(np.float64) for ind in result.pop])
-                  for result in results]
+        pops_x = [_pop_x(result.pop) for result in results]
         pops_x_f = [self._encoder.genetic_to_ml(pops_x[i], initial_states[i])
                     for i in range(len(results))]
         if len({p.shape for p in pops_x_f}) == 1:

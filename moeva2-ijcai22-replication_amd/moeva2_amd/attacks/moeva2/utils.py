@@ -3,6 +3,8 @@ from typing import List
 
 import numpy as np
 
+from .result_process import History, Population
+
 ONE_HOT_ENCODE_KEY = "ohe"
 
 
@@ -51,14 +53,24 @@ def get_one_hot_encoding_constraints(type_mask, x):
     return np.sum(np.abs(1 - vals), axis=1)
 
 
+def _pop_x(pop):
+    """One state's final genes (P, V) fp64: the engine's Population hands its array over,
+    anything else is stacked individual by individual as utils.py:59-61 does."""
+    if isinstance(pop, Population):
+        return np.asarray(pop._X, dtype=np.float64)
+    return np.array([ind.X.astype(np.float64) for ind in pop])
+
+
 def results_to_numpy_results(results: List, encoder):
     """utils.py:57-67 -> (n_states, pop_size, n_features)."""
     initial_states = [r.initial_state for r in results]
-    pops_x = [np.array([ind.X.astype(np.float64) for ind in r.pop]) for r in results]
+    pops_x = [_pop_x(r.pop) for r in results]
     return np.array([encoder.genetic_to_ml(pops_x[i], initial_states[i])
                      for i in range(len(results))])
 
 
 def results_to_history(results: List):
-    """utils.py:70-76: drop the initial-population entry."""
+    """utils.py:70-76: drop the initial-population entry -> (n_states, n_gen - 1, O, w)."""
+    if results and all(isinstance(r.history, History) for r in results):
+        return np.stack([r.history.offspring_rows() for r in results])
     return np.array([[g.tolist() for i, g in enumerate(r.history) if i > 0] for r in results])

@@ -775,6 +775,108 @@ def test_gene_layout_is_the_jobs_not_the_batchs():
         m.generate(X, 1, return_device=True, gene_layout=lay0)
 
 
+def test_gene_layout_request_applies_to_one_binding():
+    """mv_set_gene_layout applies to the NEXT mv_set_states only: after a batch
+    bound with a job's layout, a DefaultProblem on the same shared engine binds a state the
+    job never held in its own derived layout (a stale request would leave out a gene that
+    state can change and refuse it).  A refused request leaves the previous binding intact."""
+    from moeva2_amd._native import NativeError
+    from moeva2_amd.attacks.moeva2.default_problem import DefaultProblem
+    from moeva2_amd.attacks.moeva2.feature_encoder import get_encoder_from_constraints
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2
+
+    name = "botnet"
+    c = make_constraints(name)
+    p = Project(name)
+    sc = make_scaler(name)
+    m = Moeva2(os.path.join(RES, PROJECTS[name][1]), c, ml_scaler=sc, norm=2, n_gen=3,
+               n_pop=40, n_offsprings=20, seed=7)
+    X = p.x[:6].copy()
+    lay0 = m.gene_layout(X)
+    g = int(np.where(~lay0)[0][0])
+    f = int(np.where(p.lay.mutable_mask)[0][g])
+    x_new = X[5].copy()
+    x_new[f] += 0.5  # gene g is no longer fixed in this state
+    m.generate(X[:3], 1, return_device=True, gene_layout=lay0)
+    eng = m.last_engine
+    clf = m._get_classifier()
+    enc = get_encoder_from_constraints(c, x_new)
+    prob = DefaultProblem(x_new, clf, 1, enc, c, True, ml_scaler=sc, norm=2)
+    assert prob._engine is eng  # the shared engine
+    rng = np.random.default_rng(3)
+    xg = enc.ml_to_genetic(x_new[None])[0]
+    lo, hi = enc.get_min_max_genetic()
+    rows = np.clip(xg + rng.normal(0, 1, (8, xg.shape[0])) * (hi - lo) * 0.01, lo, hi)
+    rows[:, [t != "real" for t in enc.get_type_mask_genetic()]] = np.rint(
+        rows[:, [t != "real" for t in enc.get_type_mask_genetic()]])
+    F_shared = prob.evaluate(rows)
+    assert eng.stored_genes()[g]  # derived from x_new, not the batch's request
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, load_model
+
+    clf2 = Classifier(load_model(os.path.join(RES, PROJECTS[name][1])))  # a fresh engine
+    prob2 = DefaultProblem(x_new, clf2, 1, get_encoder_from_constraints(c, x_new), c, True,
+                           ml_scaler=sc, norm=2)
+    assert prob2._engine is not eng
+    np.testing.assert_array_equal(F_shared, prob2.evaluate(rows))
+    # a refused request: the previous binding (x_new) stays bound and usable
+    eng.set_gene_layout(lay0)
+    with pytest.raises(NativeError, match="not fixed"):
+        eng.set_states(x_new[None], *[a[None] for a in c.get_feature_min_max(x_new)], 1)
+    assert eng.B == 1
+    genes = torch.from_numpy(rows).cuda()[None]
+    F = torch.empty((1, rows.shape[0], 3), dtype=torch.float64, device="cuda")
+    eng.evaluate(genes, F)
+    np.testing.assert_array_equal(F[0].cpu().numpy(), F_shared)
+
+
+@pytest.mark.parametrize("name,G,hist", [("botnet", 25, "reduced"), ("lcld", 12, "full"),
+                                         ("lcld", 1, "reduced")])
+def test_generate_results_front_and_history(name, G, hist):
+    """Moeva2.generate's results from the device: res.pop = the final population, res.X /
+    res.F = its non-dominated members computed on the device (mv_attack_front), bit-identical
+    to the host relation (pareto_operation.py:35-51 as a numpy broadcast) on the same final
+    F; res.history = mv_attack_history's rows entry by entry; the results pickle (the
+    driver's legacy results_{hash}.npy) and convert (results_to_history) like lists."""
+    import pickle
+
+    from moeva2_amd.attacks.moeva2.moeva2 import Moeva2, _non_dominated
+    from moeva2_amd.attacks.moeva2.utils import results_to_history
+
+    c = make_constraints(name)
+    p = Project(name)
+    m = Moeva2(os.path.join(RES, PROJECTS[name][1]), c, ml_scaler=make_scaler(name), norm=2,
+               n_gen=G, n_pop=40, n_offsprings=20, save_history=hist, seed=5)
+    X = p.x[:7]
+    res = m.generate(X, 1)
+    g_d, F_d, h_d = m.generate(X, 1, return_device=True)  # the same attack (same seed)
+    genes, F, hh = g_d.cpu().numpy(), F_d.cpu().numpy(), h_d.cpu().numpy()
+    P, O = 43, 20
+    partial = 0
+    for b, r in enumerate(res):
+        np.testing.assert_array_equal(r.pop.get("X"), genes[b])
+        np.testing.assert_array_equal(np.stack([ind.F for ind in r.pop]), F[b])
+        nd = _non_dominated(F[b])
+        partial += int(not nd.all())
+        np.testing.assert_array_equal(r.X, genes[b][nd])
+        np.testing.assert_array_equal(r.F, F[b][nd])
+        assert len(r.history) == G
+        np.testing.assert_array_equal(r.history[0], hh[b, :P])
+        np.testing.assert_array_equal(r.history[-1], hh[b, P + (G - 2) * O:] if G > 1
+                                      else hh[b, :P])
+        assert r.pareto.shape == (0, genes.shape[2])
+    if G == 1:
+        assert partial == 0  # P copies of the initial state: none dominates another
+    ref_hist = np.array([[g.tolist() for i, g in enumerate(list(r.history)) if i > 0]
+                         for r in res])  # utils.py:70-76 on plain lists
+    if G > 1:
+        np.testing.assert_array_equal(results_to_history(res), ref_hist)
+    back = pickle.loads(pickle.dumps(res))
+    for r0, r1 in zip(res, back):
+        np.testing.assert_array_equal(r0.X, r1.X)
+        np.testing.assert_array_equal(r0.pop.get("X"), r1.pop.get("X"))
+        np.testing.assert_array_equal(r0.history[G // 2], r1.history[G // 2])
+
+
 def test_device_buffers_of_another_gpu_are_refused():
     """Entry points check that their buffers live on the engine's GPU (api.cpp on_device):
     a one-GPU box can only show that buffers of the engine's own device pass and that the
