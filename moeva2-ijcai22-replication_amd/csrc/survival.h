@@ -45,7 +45,8 @@ struct SurvLds {
   double4* Uf;      // [R+3] the same as double4 (association pre-filter)
   double* dist;     // [N]
   double* red;      // [waves*16] reduction scratch
-  double* scal;     // [40] ideal(3) worst(3) wpop(3) wfront(3) nadir(3) ext(9) prev ext(9)
+  double* scal;     // [40] ideal(3) worst(3) wpop(3) . prev ext(9) at 24
+  double* wsc;      // [waves*16] each wave's own wfront(3) nadir(3) ext(9)
   unsigned long long* dom;     // [N*NW]
   unsigned long long* ranked;  // [NW]
   unsigned long long* cur;     // [NW]
@@ -109,7 +110,7 @@ constexpr int NICHE_SORT_MIN = 256;
 
 // Byte offsets of the survival workspace inside the dynamic LDS block.
 struct SurvOff {
-  unsigned F, ref, U, Uf, dist, red, scal, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
+  unsigned F, ref, U, Uf, dist, red, scal, wsc, dom, ranked, cur, I, pos, front_of, slot, niche, memb,
       key, surv, sel, fstart, count, remain, csr_off, csr, cand, ckey, iscal, sortk, perm,
       dmin, lround, ptab, total;
 };
@@ -143,6 +144,7 @@ __host__ __device__ __forceinline__ SurvOff surv_offsets(int N, int R, int Pperm
   TAKE(dist, (size_t)N * 8)
   TAKE(red, ((threads ? threads : surv_threads(N)) / 64) * 16 * 8)
   TAKE(scal, 40 * 8)
+  TAKE(wsc, ((threads ? threads : surv_threads(N)) / 64) * 16 * 8)
   TAKE(dom, dom_lds ? (size_t)N * NW * 8 : 0)
   TAKE(ranked, NW * 8)
   TAKE(cur, NW * 8)
@@ -387,6 +389,14 @@ __device__ __forceinline__ void tournament(int P, int O_next, uint64_t seed, uin
 // position is still inside the genes is finished by its lane 3, serially (2 % of the rows);
 // more than PLAN_MUT stored mutations set the overflow flag.  par: the tournament's parents
 // (LDS, 2 per mating); geo / cmap / ginfo: LDS.
+// MV_PLAN_CAP (checks / test builds only): the stored mutations a plan row may hold before
+// it is flagged as overflowing (default PLAN_MUT).  A small cap (`make planovf`: 1) sends most
+// mutated rows through k_genc's overflow paths, which a PLAN_MUT of 8 reaches about once per
+// million rows, so their bit-parity can be tested (tests/test_gpu_parity.py).
+#ifndef MV_PLAN_CAP
+#define MV_PLAN_CAP PLAN_MUT
+#endif
+static_assert(MV_PLAN_CAP >= 1 && MV_PLAN_CAP <= PLAN_MUT, "plan cap within the plan's slots");
 template <int T>
 __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, const int gen,
                                                const int* par, int* cxs, const uint32_t* geo,
@@ -439,8 +449,8 @@ __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, c
     };
     if (stored) put(slot, cq, uq);
     if (live && q == 3) {  // the row's count (and the rare rest of its walk), then its header
-      int cnt = __popc(grp), ovf = 0;
-      if (hit) {
+      int cnt = __popc(grp), ovf = cnt > MV_PLAN_CAP ? 1 : 0;
+      if (hit && !ovf) {
         int p = pos;
         for (int j = 4;; ++j) {
           const u32x4 w = rng.draw((uint32_t)(i * MUT_J + j), (uint32_t)gen, TAG_MUT_MASK);
@@ -448,7 +458,7 @@ __device__ __forceinline__ void variation_plan(const SurvArgs& a, const int b, c
           if (p >= Vr) break;
           const int g = cmap[p];
           if (g < 0) continue;
-          if (cnt == PLAN_MUT) {
+          if (cnt >= MV_PLAN_CAP) {
             ovf = 1;
             break;
           }
@@ -486,6 +496,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   L.dist = (double*)(smem + o.dist);
   L.red = (double*)(smem + o.red);
   L.scal = (double*)(smem + o.scal);
+  L.wsc = (double*)(smem + o.wsc);
   if (NWMAX * 64 > SURV_NLDS)
     L.dom = a.dom_g + (size_t)b * a.dom_stride;
   else
@@ -516,9 +527,11 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
   double* ideal = L.scal;
   double* worst = L.scal + 3;
   double* wpop = L.scal + 6;
-  double* wfront = L.scal + 9;
-  double* nadir = L.scal + 12;
-  double* ext = L.scal + 15;  // 9
+  // the front's worst point, the nadir and the extremes: every wave computes the same bits
+  // (below) into its OWN copy and reads only that one, so no two waves write one LDS word
+  double* wfront = L.wsc + (tid >> 6) * 16;
+  double* nadir = wfront + 3;
+  double* ext = wfront + 6;  // 9
   double* pext = L.scal + 24;  // 9: the carried extremes, staged at entry
   const int has_ext = a.has_extreme[b] != 0;
   // carried ideal / worst, loaded at entry so their latency overlaps the F load
@@ -840,9 +853,9 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     __syncthreads();
     PHASE(22)
-    // lane 0 of every wave: the same combination and nadir, written to the same LDS words
-    // (identical bits); a wave reads back only what it wrote itself (LDS is in order within
-    // a wave) until the next barrier.  (Computed by one lane, in the shape of a single-
+    // lane 0 of every wave: the same combination and nadir, written to the wave's own copy
+    // (wsc; identical bits in every copy), which only that wave reads (LDS is in order
+    // within a wave).  (Computed by one lane, in the shape of a single-
     // thread block, the kernel keeps its register count: 79 VGPRs, 3 workgroups per CU.)
     if (lane == 0) {
       for (int i = 0; i < 3; ++i) {

@@ -608,6 +608,53 @@ def _attack(name, X, n_gen, seed, hist=0, P=23, O=10, mode="auto", crossover="tw
     return eng, g, F, h, ref
 
 
+PLANOVF_LIB = os.path.join(os.path.dirname(RES), "lib", "libmoeva_mi355x_planovf.so")
+
+
+@pytest.mark.parametrize("cx", ["two_point", "sbx"])
+def test_plan_overflow_paths_bit_exact(cx, tmp_path):
+    """k_genc's plan-overflow paths (a row with more stored mutations than the
+    variation plan holds: two-point rows are redone through the OVF branch, SBX rows through
+    mutate_row_full) are reached about once per million rows with PLAN_MUT = 8.  The
+    plan-overflow build (`make planovf`: MV_PLAN_CAP = 1) flags every row with two or more
+    stored mutations -- about a quarter of the rows at one expected mutation per row -- so
+    those paths carry the attack.  Its populations must be bit-identical to the default
+    build's and to the oracle's engine-order attack (oracle/device_order.py)."""
+    import subprocess
+    import sys
+
+    from moeva2_amd.problem import build_device_program
+    from oracle import device_order as do
+
+    if not os.path.exists(PLANOVF_LIB):
+        pytest.fail(f"{PLANOVF_LIB} missing: build it with `make -C "
+                    "moeva2-ijcai22-replication_amd/csrc planovf` (__graft_entry__.build())")
+    name, B, G, P, O = "botnet", 4, 6, 43, 20
+    out = str(tmp_path / "planovf.npz")
+    env = dict(os.environ, MOEVA_MI355X_LIB=PLANOVF_LIB)
+    runner = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "planovf_run.py")
+    subprocess.run([sys.executable, runner, out, name, str(B), str(G), str(P), str(O), cx],
+                   env=env, check=True, timeout=240)
+    d = np.load(out)
+    p = Project(name)
+    X = p.x[:B]
+    eng, g, F, _, ref = _attack(name, X, G, 77, P=P, O=O, crossover=cx)
+    np.testing.assert_array_equal(d["genes"], g.cpu().numpy())
+    np.testing.assert_array_equal(d["F"], F.cpu().numpy())
+    c = make_constraints(name)
+    codes = build_device_program(c).op_code
+    fixed = _fixed_features(p, eng.stored_genes())
+
+    def ev(prob, genes, return_g=False):
+        return do.evaluate_device_order(prob, genes, codes, return_g, fixed=fixed)
+
+    for b in (0, B - 1):
+        r = mo.run_attack(p.problem(X[b]), ref, G, P, O, 77, crossover_kind=cx,
+                          evaluate_fn=ev, pow_fn=do.det_pow)
+        np.testing.assert_array_equal(d["genes"][b], r.pop_X)
+        np.testing.assert_array_equal(d["F"][b], r.pop_F)
+
+
 def mo_ref_dirs(n):
     from moeva2_amd.attacks.moeva2.ref_dirs import riesz_energy_dirs
 
