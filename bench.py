@@ -39,6 +39,12 @@ WORKLOADS = {
                               model="models/botnet/nn.npz", scaler="models/botnet/scaler.npz",
                               x="data/botnet/x_candidates_common.npy", n_pop=200, n_off=100,
                               n_gen=1000, norm=2, history="reduced"),
+    # the per-GPU share of configs[1] under 8-GPU strong scaling (387 / 8 -> 48 states)
+    "rq1.botnet.static.48": dict(project="botnet", features="data/botnet/features.csv",
+                                 constraints="data/botnet/constraints.csv",
+                                 model="models/botnet/nn.npz", scaler="models/botnet/scaler.npz",
+                                 x="data/botnet/x_candidates_common.npy", n_pop=200, n_off=100,
+                                 n_gen=1000, norm=2, history="reduced", n_states=48),
     "rq1.lcld.static": dict(project="lcld", features="data/lcld/features.csv",
                             constraints="data/lcld/constraints.csv", model="models/lcld/nn.npz",
                             scaler="models/lcld/scaler.npz",

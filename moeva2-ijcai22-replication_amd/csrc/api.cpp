@@ -723,6 +723,7 @@ static RowsArgs base_rows(const mv_engine* e, bool attack) {
   a.state_keys = e->state_keys;
   a.key0 = e->key0;
   a.do_eval = 1;
+  a.states_all = e->B;
   a.p.mlp_bf16 = e->has_model && e->mlp_bf16;
   return a;
 }
@@ -1305,7 +1306,7 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
     // sub-phase marks (cycles since phase 0): 21/22 extremes (ASF loop, combine), 16..20
     // niching (keys, member lists, ranks, levels, round keys)
     std::fprintf(stderr, " | t:");
-    for (int k : {3, 21, 22, 4, 5, 10, 6, 16, 17, 18, 19, 20, 7}) {
+    for (int k : {3, 21, 22, 25, 26, 4, 5, 10, 6, 16, 17, 18, 19, 20, 7}) {
       double t = 0.0;
       for (int b = 0; b < e->B; ++b) t += (double)(ph[(size_t)b * 32 + k] - ph[(size_t)b * 32]);
       std::fprintf(stderr, " %d=%.0f", k, t / e->B);

@@ -151,6 +151,7 @@ struct RowsArgs {
   DStates s;
   int n;                    // rows per state
   int total;                // B * n
+  int states_all;           // the attack's states over all its state groups (row chunking)
   int mode;                 // 0: genes given; 1: crossover + mutation from parents
   const double* genes_in;   // mode 0: [B][in_rows][V]; mode 1: parent pool [B][in_rows][V]
   int in_rows;              // rows per state in genes_in

@@ -1932,6 +1932,32 @@ static int vary_rows_per_wg(int n) {
   return best;
 }
 
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  (void)hipGetLastError();
+  return cus;
+}
+
+// Small attacks (states_all x chunks below four workgroups per CU, k_genc's occupancy): the
+// chunks shrink -- down to one row per wave -- until the row launches fill the chip.  Each
+// chunk repeats the workgroup prologue, but with few states the CUs would idle instead, and a
+// generation's row-kernel latency is one chunk's (e.g. 48 botnet states, 8-GPU strong scaling
+// of configs[1]: 240 workgroups of 20 rows -> 1,200 of 4).  Results do not depend on the
+// chunking (every draw is keyed by the row inside its state).
+static int vary_rows_per_wg(int n, int states_all) {
+  int best = vary_rows_per_wg(n);
+  static const bool env = std::getenv("MV_VARY_ROWS") != nullptr;
+  if (env || states_all <= 0) return best;
+  static const int target = 4 * device_cus();
+  if ((long long)states_all * ((n + best - 1) / best) >= target) return best;
+  const int c = (target + states_all - 1) / states_all;  // chunks per state wanted
+  const int r = (n + c - 1) / c;
+  return r < VARY_W ? (best < VARY_W ? best : VARY_W) : (r < best ? r : best);
+}
+
 static int vary_nt(const DProblem& p) {
   const int m = p.V > p.Dm4 ? p.V : p.Dm4;
   const int nt = (m + 63) / 64;
@@ -2055,7 +2081,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
   if (use_narrow(a)) return launch_narrow(a, slot, gen, hist_row0, stream);
   if (use_genc(a)) {
     const int B = a.total / a.n;
-    const int rw = vary_rows_per_wg(a.n);
+    const int rw = vary_rows_per_wg(a.n, a.states_all);
     const dim3 grid(B * ((a.n + rw - 1) / rw));
     const int nt = genc_nt(a.p);
     const VaryOff o = vary_offsets(a.p);
@@ -2076,7 +2102,7 @@ hipError_t launch_gen(const RowsArgs& a, int slot, int gen, int hist_row0, hipSt
     return genc_go<16>(grid, lds, stream, slot, gen, hist_row0, rw, sbx, slim);
   }
   const int B = a.total / a.n;
-  const int rw = vary_rows_per_wg(a.n);
+  const int rw = vary_rows_per_wg(a.n, a.states_all);
   const dim3 grid(B * ((a.n + rw - 1) / rw));
   const int nt = vary_nt(a.p);
   const bool ident = a.p.ident != 0;
@@ -2104,7 +2130,7 @@ hipError_t launch_cons(const RowsArgs& a, int slot, int hist_row0, hipStream_t s
   if (use_narrow(a)) return hipSuccess;  // done by k_narrow in launch_gen
   if (use_genc(a)) return hipSuccess;    // done by k_genc in launch_gen
   const int B = a.total / a.n;
-  const int rw = vary_rows_per_wg(a.n);
+  const int rw = vary_rows_per_wg(a.n, a.states_all);
   const dim3 grid(B * ((a.n + rw - 1) / rw));
   const int nt = vary_nt(a.p);
   const size_t lds = cons_lds_total(vary_offsets(a.p));

@@ -216,6 +216,57 @@ __device__ __forceinline__ bool arg_better(double v, int i, double bv, int bi) {
 
 // Ordered stream compaction of the indices i in [0, n) with pred(i) into out[base..].
 // Returns the count (uniform).  Uses red scratch as int[4+1].
+// One row j = j0 + U of a dominance work item against the wave's 64 rows i (lane = i), with
+// the relation of pareto_operation.py:35-51: lt = F_i < F_j in some objective, ng = F_i > F_j
+// in none (ULE: a NaN padding row compares false both ways).  The compares' lane masks stay
+// in SGPRs (v_cmp -> s_or / s_and, no bool -> VGPR -> mask round trip): m = lt & ng (lanes i
+// that dominate j) goes to lane U of mine with v_writelane (immediate lane, so no lane-select
+// hazard), d = ~(lt | ng) (j dominates lane i) sets bit U of the lane's acc.
+template <int U>
+__device__ __forceinline__ unsigned writelane_u(unsigned old, unsigned v) {
+  unsigned r = old;
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(r) : "s"(v), "i"(U));
+  return r;
+}
+// lanes set in the uniform mask m take b, the others a (one v_cndmask on the SGPR pair)
+__device__ __forceinline__ unsigned select_mask(unsigned a, unsigned b, unsigned long long m) {
+  unsigned r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+template <int U, int NU, class Acc>
+struct DomRow {
+  __device__ __forceinline__ static void run(double fi0, double fi1, double fi2, const double* fj,
+                                             unsigned& mlo, unsigned& mhi, Acc& acc, int lane) {
+    const double g0 = fj[U * 3], g1 = fj[U * 3 + 1], g2 = fj[U * 3 + 2];
+    constexpr int OLT = 4, ULE = 13;  // llvm FCmp predicates: ordered <, unordered or <=
+    const unsigned long long lt = __builtin_amdgcn_fcmp(fi0, g0, OLT) |
+                                  __builtin_amdgcn_fcmp(fi1, g1, OLT) |
+                                  __builtin_amdgcn_fcmp(fi2, g2, OLT);
+    const unsigned long long ng = __builtin_amdgcn_fcmp(fi0, g0, ULE) &
+                                  __builtin_amdgcn_fcmp(fi1, g1, ULE) &
+                                  __builtin_amdgcn_fcmp(fi2, g2, ULE);
+    const unsigned long long m = lt & ng;
+    const unsigned long long d = ~(lt | ng);
+    mlo = writelane_u<U>(mlo, (unsigned)m);
+    mhi = writelane_u<U>(mhi, (unsigned)(m >> 32));
+    if constexpr (U < 32) {
+      const unsigned lo = (unsigned)acc;
+      acc = (acc & ~(Acc)0xFFFFFFFFu) | (Acc)select_mask(lo, lo | (1u << U), d);
+    } else {
+      const unsigned hi = (unsigned)((unsigned long long)acc >> 32);
+      acc = (acc & (Acc)0xFFFFFFFFu) |
+            ((Acc)select_mask(hi, hi | (1u << (U - 32)), d) << 32);
+    }
+    DomRow<U + 1, NU, Acc>::run(fi0, fi1, fi2, fj, mlo, mhi, acc, lane);
+  }
+};
+template <int NU, class Acc>
+struct DomRow<NU, NU, Acc> {
+  __device__ __forceinline__ static void run(double, double, double, const double*, unsigned&,
+                                             unsigned&, Acc&, int) {}
+};
+
 template <int T, class Pred>
 __device__ __forceinline__ int block_compact(int n, Pred pred, int* out, int base, int* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -655,16 +706,10 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       const double fi0 = L.F[i * 3 + 0], fi1 = L.F[i * 3 + 1], fi2 = L.F[i * 3 + 2];
       const int j0 = qj * 64;
       const double* fj = L.F + j0 * 3;
-      unsigned long long mine = 0ull, acc = 0ull;
-#pragma unroll 4
-      for (int u = 0; u < 64; ++u) {
-        const double g0 = fj[u * 3], g1 = fj[u * 3 + 1], g2 = fj[u * 3 + 2];
-        const bool lt = (fi0 < g0) | (fi1 < g1) | (fi2 < g2);
-        const bool gt = (fi0 > g0) | (fi1 > g1) | (fi2 > g2);
-        const unsigned long long m = __ballot(lt && !gt);
-        mine = lane == u ? m : mine;
-        acc |= (gt && !lt) ? (1ull << u) : 0ull;
-      }
+      unsigned mlo = 0u, mhi = 0u;
+      unsigned long long acc = 0ull;
+      DomRow<0, 64, unsigned long long>::run(fi0, fi1, fi2, fj, mlo, mhi, acc, lane);
+      const unsigned long long mine = ((unsigned long long)mhi << 32) | mlo;
       if (j0 + lane < N) L.dom[(size_t)qi * N + j0 + lane] = mine;
       if (qi != qj && i < N) L.dom[(size_t)qj * N + i] = acc;
     }
@@ -687,17 +732,9 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       const double fi0 = L.F[i * 3 + 0], fi1 = L.F[i * 3 + 1], fi2 = L.F[i * 3 + 2];
       const int j0 = qj * 64 + qq * 16;
       const double* fj = L.F + j0 * 3;
-      unsigned long long mine = 0ull;
-      unsigned acc = 0u;
-#pragma unroll 4
-      for (int u = 0; u < 16; ++u) {
-        const double g0 = fj[u * 3], g1 = fj[u * 3 + 1], g2 = fj[u * 3 + 2];
-        const bool lt = (fi0 < g0) | (fi1 < g1) | (fi2 < g2);
-        const bool gt = (fi0 > g0) | (fi1 > g1) | (fi2 > g2);
-        const unsigned long long m = __ballot(lt && !gt);
-        mine = lane == u ? m : mine;
-        acc |= (gt && !lt) ? (1u << u) : 0u;
-      }
+      unsigned mlo = 0u, mhi = 0u, acc = 0u;
+      DomRow<0, 16, unsigned>::run(fi0, fi1, fi2, fj, mlo, mhi, acc, lane);
+      const unsigned long long mine = ((unsigned long long)mhi << 32) | mlo;
       if (lane < 16 && j0 + lane < N)
         L.dom[(size_t)qi * N + j0 + lane] = mine;
       if (qi != qj && i < N) dom16[((size_t)qj * N + i) * 4 + qq] = (unsigned short)acc;
@@ -853,24 +890,40 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     __syncthreads();
     PHASE(22)
-    // lane 0 of every wave: the same combination and nadir, written to the wave's own copy
-    // (wsc; identical bits in every copy), which only that wave reads (LDS is in order
-    // within a wave).  (Computed by one lane, in the shape of a single-
-    // thread block, the kernel keeps its register count: 79 VGPRs, 3 workgroups per CU.)
-    if (lane == 0) {
+    // every wave: the same combination of the waves' partials (lane w holds wave w's; a
+    // lexicographic (value, index) argmin and a NaN-propagating max, both independent of the
+    // combination order, so every wave gets the same bits) and then, on lane 0, the
+    // extremes and the nadir, written to the wave's own copy (wsc), which only that wave
+    // reads (LDS is in order within a wave).
+    double cw[3];
+    int cix[3];
+    {
+      constexpr int NWV = T / 64;
+      static_assert(NWV <= 16, "survival combine: at most 16 waves");
+      const bool has = lane < NWV;
       for (int i = 0; i < 3; ++i) {
-        double v = L.red[i];
-        int ix = (int)L.red[3 + i];
-        double w = L.red[6 + i];
-        for (int ww = 1; ww < T / 64; ++ww) {
-          const double ov = L.red[ww * 16 + i];
-          const int oi = (int)L.red[ww * 16 + 3 + i];
+        double v = has ? L.red[lane * 16 + i] : __builtin_inf();
+        int ix = has ? (int)L.red[lane * 16 + 3 + i] : INT_MAX;
+        double w = has ? L.red[lane * 16 + 6 + i] : -__builtin_inf();
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          const double ov = __shfl_xor(v, off, 16);
+          const int oi = __shfl_xor(ix, off, 16);
+          const double ow = __shfl_xor(w, off, 16);
           if (ov < v || (ov == v && oi < ix)) {
             v = ov;
             ix = oi;
           }
-          w = max_prop(w, L.red[ww * 16 + 6 + i]);
+          w = max_prop(w, ow);
         }
+        cix[i] = ix;
+        cw[i] = w;
+      }
+    }
+    if (lane == 0) {
+      for (int i = 0; i < 3; ++i) {
+        const int ix = cix[i];
+        const double w = cw[i];
         wfront[i] = w;
         double row[3];
         if (ix < ne) {
@@ -885,6 +938,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     }
     wave_sync();
+    PHASE(25)
     if (lane == 0) {
       // nadir (get_nadir_point with the call-site argument swap)
       double M[3][3], plane[3] = {1.0, 1.0, 1.0};
@@ -922,6 +976,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
       }
     }
     wave_sync();
+    PHASE(26)
   }
   PHASE(4)
 
