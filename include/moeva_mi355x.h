@@ -290,7 +290,8 @@ int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations);
 int mv_get_row_kernel(mv_engine* e, int32_t* kind);
 /* The classifier kernel an attack generation runs: 0 = k_mlp (one tile of rows per
  * workgroup, any widths), 1 = k_mlp2 reading the child genes (no fp32 ML row is written),
- * 2 = k_mlp2 reading the fp32 ML rows, 4 = k_mlpw (bf16 weights), -1 = no device classifier
+ * 2 = k_mlp2 reading the fp32 ML rows, 4 = k_mlpw (bf16 weights), 5 = k_mlpw32 (fp32 wide
+ * nets: 64-row tiles, one activation buffer), -1 = no device classifier
  * (3, the retired k_mlp2x, is no longer returned).
  * Lets a profiler price the ML-row bytes of the row kernel and the classifier. */
 int mv_get_mlp_kernel(mv_engine* e, int32_t* kind);

@@ -431,7 +431,10 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
     // xml_direct: k_mlp2 builds its layer-0 tiles from the child genes (MV_XML: the fp32
     // ML rows written by the row kernel + k_mlp2, A/B only)
     p.xml_direct = p.mlp2 && p.ident && !std::getenv("MV_XML");
-    for (int l = 0; l + 1 < hm->n_layers && p.mlp2; ++l) {
+    // the same packing feeds k_mlpw32 (fp32 wide nets): every hidden width a multiple of 16
+    bool pack16 = true;
+    for (int l = 1; l < hm->n_layers; ++l) pack16 &= hm->dims[l] % 16 == 0;
+    for (int l = 0; l + 1 < hm->n_layers && pack16; ++l) {
       const int Kl = l == 0 ? p.Dm4 : hm->dims[l], Nl = hm->dims[l + 1];
       const float* src = l == 0 ? w1m.data() : hm->W[l].data();  // [Kl][Nl] row-major
       std::vector<float> wp((size_t)Kl * Nl, 0.f);

@@ -115,7 +115,7 @@ struct DProblem {
   // k_mlp2 weights: per hidden layer l, [K_l/16][N_l][16] (16 consecutive k of one output
   // column contiguous; K_0 = Dm4, K_l = dims[l]), so one dwordx4 load is a lane's B operand
   // for four 16x16x4 MFMA k-steps
-  const float* Wp[MAX_LAYERS];
+  const float* Wp[MAX_LAYERS];  // also k_mlpw32's (fp32 wide nets); NULL unless packed
   int mlp2;               // hidden widths fit k_mlp2 (multiples of 16, <= 128)
   // bf16 perf mode (mv_set_mlp_precision, opt-in; fp32 is the parity default): the hidden
   // layers' weights as bf16 bits packed [K/32][N][32] (K zero padded to a multiple of 32:

@@ -1696,6 +1696,213 @@ __global__ __launch_bounds__(MW_T) void k_mlpw(int slot, int hist_row0) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// k_mlpw32: the fp32 (parity-mode) classifier for WIDE hidden layers (BASELINE configs[4]:
+// 756-512-512-256-2) -- 64-row persistent tiles, 8 waves, one workgroup per CU.  Exact fp32
+// products on v_mfma_f32_16x16x4f32 like k_mlp2; a 64-row fp32 activation tile of width 512
+// is 128 KiB, so there is ONE activation buffer: each layer accumulates its outputs in
+// registers, a barrier retires every wave's reads of the layer input, then the outputs
+// (bias + ReLU) overwrite it.  Per k-group of 16 a lane reads its four rows' A fragments as
+// ds_read_b128 (k = 16 kg + 4 ka + s for sub-step s, as k_mlp2's packed Wp) and CJ dwordx4
+// of the packed weights, loaded one k-group ahead; 16 CJ MFMAs per k-group.  The last
+// hidden layer folds into the final Dense from the fp32 registers (as k_mlpw) -> softmax.
+// Replaces the 32-row-tile k_mlp for this shape (each weight byte from L2 now serves 64
+// rows; the tile's MFMAs per k-group no longer wait out their loads).
+struct Mw32Lds {
+  unsigned h, part, total;
+  int hs;  // fp32 row stride of the activation buffer
+};
+__host__ __device__ inline Mw32Lds mlpw32_lds(const DProblem& p) {
+  const int nl = p.n_layers;
+  int w = p.Dm4;
+  for (int l = 1; l < nl; ++l) w = p.dims[l] > w ? p.dims[l] : w;
+  Mw32Lds L{};
+  L.hs = w + 4;  // 16-B row padding: consecutive rows start 4 banks apart
+  const unsigned head =
+      256 + (((unsigned)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~15u);
+  L.h = head;
+  L.part = L.h + (unsigned)MW_ROWS * L.hs * 4;
+  L.total = L.part + (unsigned)(MW_T / 64) * MW_ROWS * p.dims[nl] * 4;
+  return L;
+}
+// The shapes k_mlpw32 takes: every MFMA layer's K and N multiples of 16 (Wp packed), at
+// most 4 column tiles per wave (N <= 512: the 256-VGPR budget of two waves per SIMD), LDS
+// within the CU's 160 KiB.
+__host__ __device__ inline bool mlpw32_ok(const DProblem& p) {
+  if (p.n_layers < 2 || !p.Wp[0]) return false;
+  for (int l = 1; l < p.n_layers; ++l)
+    if (p.dims[l] % 16 || p.dims[l] > 512) return false;
+  return p.Dm4 % 16 == 0 && p.dims[p.n_layers] <= 8 && mlpw32_lds(p).total <= 160 * 1024;
+}
+
+template <int CJ>
+__global__ __launch_bounds__(MW_T) void k_mlpw32(int slot, int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const DProblem& p = a.p;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int il = lane & 15, ka = lane >> 4;
+  const int nl = p.n_layers;
+  const int K0 = p.Dm4;
+  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
+  const Mw32Lds L = mlpw32_lds(p);
+  const int hs = L.hs;
+  int* rowst = (int*)smem;
+  float* wl = (float*)(smem + 256);
+  float* bl = wl + Klast * nout;
+  float* H = (float*)(smem + L.h);
+  float* part = (float*)(smem + L.part);
+  for (int q = tid; q < Klast * nout; q += MW_T) wl[q] = p.W[nl - 1][q];
+  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
+  const int nq = K0 >> 2;  // float4 pieces of a layer-0 row
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r0 = tile * MW_ROWS;
+    __syncthreads();  // the previous tile's readers of rowst / H / part are done
+    if (tid < MW_ROWS) rowst[tid] = r0 + tid < a.total ? (r0 + tid) / a.n : -1;
+    // layer-0 input: the fp32 ML rows (k_genc's xml)
+    for (int idx = tid; idx < MW_ROWS * nq; idx += MW_T) {
+      const int row = idx / nq, q = idx - row * nq;
+      const int rr = r0 + row < a.total ? r0 + row : a.total - 1;
+      *(float4*)(H + row * hs + 4 * q) = *(const float4*)(a.xml + (size_t)rr * K0 + 4 * q);
+    }
+    __syncthreads();
+    for (int l = 0; l + 1 < nl; ++l) {
+      const int K = l == 0 ? K0 : p.dims[l];
+      const int N = p.dims[l + 1];
+      const int nct = N >> 4;
+      const int ng = K >> 4;
+      const float* W = p.Wp[l];
+      floatx4 acc[CJ][4];
+#pragma unroll
+      for (int j = 0; j < CJ; ++j)
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) acc[j][rt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      auto load_b = [&](int kg, float4 (&b)[CJ]) {
+        const int kc = kg < ng ? kg : ng - 1;
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) {
+          const int ct = wave + 8 * j < nct ? wave + 8 * j : nct - 1;
+          b[j] = *(const float4*)(W + ((size_t)kc * N + ct * 16 + il) * 16 + 4 * ka);
+        }
+      };
+      auto load_a = [&](int kg, float4 (&af)[4]) {
+        const int kc = kg < ng ? kg : ng - 1;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+          af[rt] = *(const float4*)(H + (rt * 16 + il) * hs + 16 * kc + 4 * ka);
+      };
+      float4 b0[CJ], af[4];
+      load_b(0, b0);
+      for (int kg = 0; kg < ng; ++kg) {
+        float4 b1[CJ];
+        load_b(kg + 1, b1);  // the next k-group's weights fly over this one's 16 CJ MFMAs
+        load_a(kg, af);
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+          for (int j = 0; j < CJ; ++j) {
+            if (wave + 8 * j < nct) {
+              const float bv = sub == 0 ? b0[j].x : sub == 1 ? b0[j].y : sub == 2 ? b0[j].z : b0[j].w;
+#pragma unroll
+              for (int rt = 0; rt < 4; ++rt) {
+                const float av = sub == 0 ? af[rt].x : sub == 1 ? af[rt].y
+                                 : sub == 2 ? af[rt].z : af[rt].w;
+                acc[j][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j][rt], 0, 0, 0);
+              }
+            }
+          }
+#pragma unroll
+        for (int j = 0; j < CJ; ++j) b0[j] = b1[j];
+      }
+      const bool last = l + 2 == nl;
+      __syncthreads();  // every wave's reads of this layer's input are done: outputs replace it
+      // + bias, ReLU; hidden outputs to LDS (fp32)
+#pragma unroll
+      for (int j = 0; j < CJ; ++j) {
+        const int ct = wave + 8 * j;
+        if (ct < nct) {
+          const int col = ct * 16 + il;
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt) {
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              const int row = rt * 16 + ka * 4 + jj;
+              float bv;
+              if (l == 0) {
+                const int s = rowst[row];
+                bv = a.s.bias1[(size_t)(s < 0 ? 0 : s) * N + col];
+              } else {
+                bv = p.bias[l][col];
+              }
+              const float v = acc[j][rt][jj] + bv;
+              acc[j][rt][jj] = v > 0.f ? v : 0.f;
+              if (!last) H[row * hs + col] = acc[j][rt][jj];
+            }
+          }
+        }
+      }
+      if (last) {
+        // the final Dense from the fp32 registers (as k_mlpw)
+        for (int c = 0; c < nout; ++c) {
+          float ps[4][4];
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) ps[rt][jj] = 0.f;
+#pragma unroll
+          for (int j = 0; j < CJ; ++j) {
+            const int ct = wave + 8 * j;
+            if (ct < nct) {
+              const float wv = wl[(ct * 16 + il) * nout + c];
+#pragma unroll
+              for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) ps[rt][jj] = fmaf(acc[j][rt][jj], wv, ps[rt][jj]);
+            }
+          }
+#pragma unroll
+          for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              float v = ps[rt][jj];
+              v += __shfl_xor(v, 1);
+              v += __shfl_xor(v, 2);
+              v += __shfl_xor(v, 4);
+              v += __shfl_xor(v, 8);
+              if (il == 0) part[(wave * MW_ROWS + rt * 16 + ka * 4 + jj) * nout + c] = v;
+            }
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < MW_ROWS) {
+      const int s = rowst[tid];
+      if (s >= 0) {
+        double z[8];
+        double mx = -__builtin_inf();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          z[c] = 0.0;
+          if (c < nout) {
+            float t = 0.f;
+            for (int w = 0; w < MW_T / 64; ++w) t += part[(w * MW_ROWS + tid) * nout + c];
+            z[c] = (double)(t + bl[c]);
+            mx = z[c] > mx ? z[c] : mx;
+          }
+        }
+        const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
+        const int i = r0 + tid - s * a.n;
+        if (a.F) {
+          const int orow = a.out_map ? a.out_map[(size_t)s * a.n + i] : i;
+          a.F[((size_t)s * a.out_rows + orow) * 3] = f1;
+        }
+        if (a.hist) a.hist[((size_t)s * a.hist_rows + hist_row0 + i) * a.hist_w] = f1;
+      }
+    }
+  }
+}
+
 // Classifier.predict_proba: 16 RT rows per workgroup, full-width first layer.
 template <int MAXCT, int RT = 2>
 __global__ __launch_bounds__(EVAL_T) void k_predict(MlpArgs a) {
@@ -2229,13 +2436,36 @@ static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   return hipGetLastError();
 }
 
+template <int CJ>
+static hipError_t mlpw32_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  static bool configured = false;
+  if (!configured) {
+    allow_lds(k_mlpw32<CJ>);
+    configured = true;
+  }
+  const size_t lds = mlpw32_lds(a.p).total;
+  const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
+  const int grid = ntiles < cu_count() ? ntiles : cu_count();  // one workgroup per CU
+  hipLaunchKernelGGL((k_mlpw32<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
+  return hipGetLastError();
+}
+
+// fp32 wide classifiers (hidden widths above k_mlp2's 128) on k_mlpw32; MV_MLPW32=0 keeps
+// the 32-row-tile k_mlp (A/B)
+static bool use_mlpw32(const DProblem& p) {
+  static const bool off = std::getenv("MV_MLPW32") && std::getenv("MV_MLPW32")[0] == '0';
+  return !off && !p.mlp_bf16 && mlpw32_ok(p);
+}
+
 // launch_mlp's choice for a problem: 0 k_mlp, 1 k_mlp2 reading the genes (xml_direct),
-// 2 k_mlp2 reading the fp32 ML rows, 4 k_mlpw (bf16), -1 no model (3, k_mlp2x, was retired)
+// 2 k_mlp2 reading the fp32 ML rows, 4 k_mlpw (bf16), 5 k_mlpw32 (fp32 wide), -1 no model
+// (3, k_mlp2x, was retired)
 int mlp_kernel_kind(const DProblem& p) {
   if (p.n_layers == 0) return -1;
   if (p.mlp2 && !std::getenv("MV_MLP_V1") && !(p.mlp_bf16 && std::getenv("MV_MLPW")))
     return p.xml_direct ? 1 : 2;
   if (p.mlp_bf16 && mlpw_lds(p).total <= 160 * 1024 && !std::getenv("MV_MLPW_OFF")) return 4;
+  if (use_mlpw32(p)) return 5;
   return 0;
 }
 
@@ -2254,6 +2484,12 @@ hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t st
     return hm <= 128 ? mlpw_go<1>(a, slot, hist_row0, stream)
                      : hm <= 256 ? mlpw_go<2>(a, slot, hist_row0, stream)
                                  : mlpw_go<4>(a, slot, hist_row0, stream);
+  }
+  if (use_mlpw32(a.p)) {
+    const int hm = max_hidden(a.p.dims, a.p.n_layers);
+    return hm <= 128 ? mlpw32_go<1>(a, slot, hist_row0, stream)
+                     : hm <= 256 ? mlpw32_go<2>(a, slot, hist_row0, stream)
+                                 : mlpw32_go<4>(a, slot, hist_row0, stream);
   }
   configure_lds_once();
   const int nl = a.p.n_layers;

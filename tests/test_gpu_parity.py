@@ -147,9 +147,9 @@ def _wide_mlp(dims=(756, 512, 512, 256, 2), seed=7):
 
 
 def test_wide_mlp_config_matches_fp32_reference():
-    """BASELINE configs[4] (synthetic.botnet.wide: 756-512-512-256-2) runs the 32-row-tile
-    k_mlp path (hidden widths > 128) in the attack and k_predict in predict_proba: f1 of
-    mv_evaluate and of Classifier.predict_proba against the fp32 numpy forward (1e-5 rel),
+    """BASELINE configs[4] (synthetic.botnet.wide: 756-512-512-256-2) runs the 64-row-tile
+    k_mlpw32 path (fp32 hidden widths > 128) in the attack and k_predict in predict_proba: f1
+    of mv_evaluate and of Classifier.predict_proba against the fp32 numpy forward (1e-5 rel),
     f2/f3 unchanged, then a short attack keeps its invariants and is deterministic."""
     from moeva2_amd.attacks.moeva2.classifier import Classifier, DenseMLPModel
     from moeva2_amd.io.tf_bundle import DenseMLP
@@ -166,6 +166,7 @@ def test_wide_mlp_config_matches_fp32_reference():
     eng = get_engine(c, clf, sc, 2)
     bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
     eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    assert eng.kernel_times()["mlp_kernel"] == "k_mlpw32"
     rng = np.random.default_rng(5)
     n = 37
     genes = np.empty((X.shape[0], n, p.lay.V))
