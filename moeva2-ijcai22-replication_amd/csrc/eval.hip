@@ -1585,18 +1585,15 @@ __global__ __launch_bounds__(MW_T) void k_mlpw(int slot, int hist_row0) {
           bf[j] = *(const bf16x8*)(W + ((size_t)sc * N + ct * 16 + il) * 32 + 8 * ka);
         }
       };
-      bf16x8 bf[CJ];
-      load_b(0, bf);
-      for (int st = 0; st < nst; ++st) {
-        bf16x8 bn[CJ];
-        load_b(st + 1, bn);
-        const int k = 32 * st + 8 * ka;
-        bf16x8 af[4];
+      auto load_a = [&](int st, bf16x8 (&af)[4]) {
+        const int k = 32 * (st < nst ? st : nst - 1) + 8 * ka;
 #pragma unroll
         for (int rt = 0; rt < 4; ++rt) {
           af[rt] = *(const bf16x8*)(in + (rt * 16 + il) * hs + (k < K ? k : 0));
           if (k >= K) af[rt] = bf16x8{};
         }
+      };
+      auto step = [&](const bf16x8 (&bf)[CJ], const bf16x8 (&af)[4]) {
 #pragma unroll
         for (int j = 0; j < CJ; ++j) {
           if (wave + 8 * j < nct) {
@@ -1605,9 +1602,24 @@ __global__ __launch_bounds__(MW_T) void k_mlpw(int slot, int hist_row0) {
               acc[j][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bf[j], acc[j][rt], 0, 0, 0);
           }
         }
-#pragma unroll
-        for (int j = 0; j < CJ; ++j) bf[j] = bn[j];
+      };
+      // two operand sets used in turn, so each k-step's loads land in the set the step after
+      // next consumes: no register rotation (a move of an in-flight load's destination makes
+      // the compiler wait vmcnt(0), which is what kept the one-step prefetch from hiding
+      // anything)
+      bf16x8 bA[CJ], bB[CJ], aA[4], aB[4];
+      load_b(0, bA);
+      load_a(0, aA);
+      int st = 0;
+      for (; st + 1 < nst; st += 2) {
+        load_b(st + 1, bB);
+        load_a(st + 1, aB);
+        step(bA, aA);
+        load_b(st + 2, bA);  // clamped past the end (an unused load on the last pair)
+        load_a(st + 2, aA);
+        step(bB, aB);
       }
+      if (st < nst) step(bA, aA);
       const bool last = l + 2 == nl;
       // + bias, ReLU in place; hidden outputs to LDS as bf16
 #pragma unroll
@@ -1704,7 +1716,8 @@ __global__ __launch_bounds__(MW_T) void k_mlpw(int slot, int hist_row0) {
 // registers, a barrier retires every wave's reads of the layer input, then the outputs
 // (bias + ReLU) overwrite it.  Per k-group of 16 a lane reads its four rows' A fragments as
 // ds_read_b128 (k = 16 kg + 4 ka + s for sub-step s, as k_mlp2's packed Wp) and CJ dwordx4
-// of the packed weights, loaded one k-group ahead; 16 CJ MFMAs per k-group.  The last
+// of the packed weights, one k-group ahead in two alternating operand sets; 16 CJ MFMAs per
+// k-group.  The last
 // hidden layer folds into the final Dense from the fp32 registers (as k_mlpw) -> softmax.
 // Replaces the 32-row-tile k_mlp for this shape (each weight byte from L2 now serves 64
 // rows; the tile's MFMAs per k-group no longer wait out their loads).
@@ -1792,18 +1805,13 @@ __global__ __launch_bounds__(MW_T) void k_mlpw32(int slot, int hist_row0) {
         for (int rt = 0; rt < 4; ++rt)
           af[rt] = *(const float4*)(H + (rt * 16 + il) * hs + 16 * kc + 4 * ka);
       };
-      float4 b0[CJ], af[4];
-      load_b(0, b0);
-      for (int kg = 0; kg < ng; ++kg) {
-        float4 b1[CJ];
-        load_b(kg + 1, b1);  // the next k-group's weights fly over this one's 16 CJ MFMAs
-        load_a(kg, af);
+      auto step = [&](const float4 (&b)[CJ], const float4 (&af)[4]) {
 #pragma unroll
         for (int sub = 0; sub < 4; ++sub)
 #pragma unroll
           for (int j = 0; j < CJ; ++j) {
             if (wave + 8 * j < nct) {
-              const float bv = sub == 0 ? b0[j].x : sub == 1 ? b0[j].y : sub == 2 ? b0[j].z : b0[j].w;
+              const float bv = sub == 0 ? b[j].x : sub == 1 ? b[j].y : sub == 2 ? b[j].z : b[j].w;
 #pragma unroll
               for (int rt = 0; rt < 4; ++rt) {
                 const float av = sub == 0 ? af[rt].x : sub == 1 ? af[rt].y
@@ -1812,8 +1820,23 @@ __global__ __launch_bounds__(MW_T) void k_mlpw32(int slot, int hist_row0) {
               }
             }
           }
-#pragma unroll
-        for (int j = 0; j < CJ; ++j) b0[j] = b1[j];
+      };
+      // two weight sets used in turn (no register rotation: see k_mlpw); the A fragments are
+      // read at each k-group's start (a second set would spill at CJ = 4)
+      float4 bA[CJ], bB[CJ], af[4];
+      load_b(0, bA);
+      int kg = 0;
+      for (; kg + 1 < ng; kg += 2) {
+        load_b(kg + 1, bB);
+        load_a(kg, af);
+        step(bA, af);
+        load_b(kg + 2, bA);  // clamped past the end (an unused load on the last pair)
+        load_a(kg + 1, af);
+        step(bB, af);
+      }
+      if (kg < ng) {
+        load_a(kg, af);
+        step(bA, af);
       }
       const bool last = l + 2 == nl;
       __syncthreads();  // every wave's reads of this layer's input are done: outputs replace it
