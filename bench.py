@@ -232,7 +232,7 @@ def data_note(w, B):
     return f"{src[w['project']]} ({how}) + {clf} and shipped scaler"
 
 
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")  # newest first: traffic measured on the current kernels wins
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")  # newest first: traffic measured on the current kernels wins
 
 
 def load_traffic(workload):

@@ -17,9 +17,9 @@ for s in $STEPS; do
   case $s in
     tests) run tests timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1
            tail -3 $O/gpu_tests.log ;;
-    prof) run prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py $BA --steps 2 --warmup 1 --no-cpu-baseline --groups 1 > $O/prof.log 2>&1
+    prof) run prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py $BA --steps 2 --warmup 1 --no-cpu-baseline --no-generate --groups 1 > $O/prof.log 2>&1
           cp $(find $O/prof -name '*kernel_stats.csv' | head -1) $O/kernel_stats.csv ;;
-    timeline) run timeline timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 1 --no-cpu-baseline --n-gen 200 > $O/tl.log 2>&1
+    timeline) run timeline timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tl -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 1 --no-cpu-baseline --no-generate --no-configs --n-gen 200 > $O/tl.log 2>&1
           python3 tools/timeline.py $(find $O/tl -name '*kernel_trace.csv' | head -1) > $O/timeline.txt 2>&1; cat $O/timeline.txt ;;
     pmc) run pmc_fetch timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --n-gen 20 --groups 1 > $O/pmc_fetch.log 2>&1
          run pmc_write timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run --output-format csv -- python3 bench.py $BA --steps 1 --warmup 0 --no-cpu-baseline --n-gen 20 --groups 1 > $O/pmc_write.log 2>&1
