@@ -374,7 +374,8 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
       // with SlotRow operands: slot j < Dm = stored mutable feature j (the wave's row buffer),
       // Dm + f = feature f of x_init (IDENT problems: k_genc's only ones)
       const int n_lane = C - n_sd;
-      p.slim = p.ident && n_lane <= 64 * OPS_REG && Dm + D < 0x4000;
+      // tol >= 0: constraints_slim's clamp (v <= tol ? 0 : v) equals the general one then
+      p.slim = p.ident && n_lane <= 64 * OPS_REG && Dm + D < 0x4000 && h.tol >= 0.0;
       std::vector<int> slot(D);
       for (int f = 0; f < D; ++f) slot[f] = Dm + f;
       for (int j = 0; j < Dm; ++j) slot[mut[j]] = j;
@@ -382,6 +383,7 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
       std::vector<double> k1(C);
       std::vector<int> sd((size_t)(n_sd > 0 ? n_sd : 1) * 4, 0);
       std::vector<unsigned> opw(C);
+      bool sd_small = true;  // every ABS_SUMDIFF side within one term per lane
       for (int k = 0; k < C; ++k) {
         k1[k] = sk[(size_t)k * 2];
         const int* ar = &sarg[(size_t)k * 4];
@@ -392,8 +394,10 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
         } else {
           opw[k] = 0u;
           for (int q = 0; q < 4; ++q) sd[(size_t)(k - n_lane) * 4 + q] = ar[q];
+          sd_small &= ar[1] - ar[0] <= 64 && ar[2] - ar[1] <= 64;
         }
       }
+      p.sd_reg = p.slim && n_sd <= SD_REG && sd_small;
       std::vector<int> spool(h.n_pool > 0 ? h.n_pool : 1, 0);
       for (int q = 0; q < h.n_pool; ++q) {
         p.slim &= h.pool[q] >= 0 && h.pool[q] < D;
@@ -405,6 +409,8 @@ static int build_problem(const HostProblem& h, const HostModel* hm, const std::v
       put(vo.s_sd, sd.data(), sd.size() * 4);
       put(vo.s_opw, opw.data(), (size_t)C * 4);
       if (std::getenv("MV_SLIM") && std::getenv("MV_SLIM")[0] == '0') p.slim = 0;  // A/B
+      if (!p.slim || (std::getenv("MV_SD_REG") && std::getenv("MV_SD_REG")[0] == '0'))
+        p.sd_reg = 0;
     }
     K((unsigned char**)&p.vblob, blob.data(), blob.size());
   }

@@ -130,8 +130,12 @@ struct DProblem {
   int xml_direct;
   // every lane op of the constraint program is DIFF or RATIO_SAFE, at most OPS_REG per lane
   // (rowops.h), plus ABS_SUMDIFF ops: k_genc's phase 2 stages the slim region S of the
-  // problem blob instead of region A (7-10 KiB less LDS per workgroup)
+  // problem blob instead of region A (7-10 KiB less LDS per workgroup); tol >= 0
   int slim;
+  // slim, with at most SD_REG ABS_SUMDIFF ops of at most 64 pool entries per side: each
+  // lane's operands of those ops are LDS addresses held in registers (rowops.h
+  // constraints_slim)
+  int sd_reg;
 };
 
 struct DStates {

@@ -372,6 +372,10 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     ftab.hhi = ftab.hlo + (size_t)a.hist_rows * a.hist_w;
   }
   const SlotRow fsrow{frow, (const double*)(smem + L.x_at), p.Dm};
+  SlimOps fso;
+  if (FUSED)
+    slim_ops(ftab, opw, kops, p.sd_reg != 0, frow, smem + L.x_at, smem + (o.s_zero - o.s_at),
+             p.Dm, lane, fso);
   if (ev && !IDENT) {  // immutable features of this wave's row buffer (written once)
     const double* s_xi = (const double*)(smem + L.x_at);
     for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
@@ -489,7 +493,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
                     : nullptr;
       double* hc = (hrow && a.hist_w > 3) ? hrow + 3 : nullptr;
       double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-      f3 = constraints_regs<false, true>(ftab, opw, kops, fsrow, lane, grow, hc);
+      f3 = constraints_slim(ftab, fso, fsrow, lane, grow, hc);
     }
     if (lane == 0) {
       double f2 = l2 ? sqrt(acc) : acc;
@@ -507,20 +511,8 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     }
     if constexpr (FUSED) wave_sync();  // the next row overwrites the row buffer
   };
-  for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
-    double x[NT];
-    if constexpr (PF2) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        x[t] = xa[t];
-        xa[t] = xb[t];
-      }
-      if (k + 2 < nrw) load_row(k + 2, xb);
-    } else {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) x[t] = xa[t];
-      if (k + 1 < nrw) load_row(k + 1, xa);
-    }
+  // the row's variation (SBX children, mutations) and finish_row, on the registers x
+  auto do_row = [&](int k, double (&x)[NT]) __attribute__((always_inline)) {
     if (sbx) {  // SBX children, then every mutation of the row
       const int i = rc.i0 + wave + VARY_W * k;
       const int nm = a.n / 2;
@@ -541,6 +533,29 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
         apply_row_mutations<NT, MUT_CAP>(x, rdl(mut_v, k) & 7, mposv, mvalv, k, lane);
     }
     finish_row(k, x);
+  };
+  if constexpr (PF2) {
+    for (int k = 0; k < nrw; ++k) {  // xa: row k, xb: row k + 1 (in flight), rotated
+      double x[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        x[t] = xa[t];
+        xa[t] = xb[t];
+      }
+      if (k + 2 < nrw) load_row(k + 2, xb);
+      do_row(k, x);
+    }
+  } else {
+    // one row in flight, two row buffers taking turns (a rotation through a copy cost ten
+    // moves per row: the copy, and the loop-carried copy back)
+    double xc[NT];
+    for (int k = 0; k < nrw; k += 2) {
+      if (k + 1 < nrw) load_row(k + 1, xc);
+      do_row(k, xa);
+      if (k + 1 >= nrw) break;
+      if (k + 2 < nrw) load_row(k + 2, xa);
+      do_row(k + 1, xc);
+    }
   }
   // Rare: rows with more than MUT_CAP mutations are redone here with every mutation (same
   // lanes, same addresses, so these stores land after the row loop's).
@@ -670,6 +685,7 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
   if (!SLIM)
     for (int f = lane; f < p.D; f += 64) xrow[f] = s_xi[f];
   const SlotRow srow{xrow, s_xi, p.Dm};
+  SlimOps so;
   OpTab tab;
   if (SLIM) {
     tab.code = nullptr;
@@ -693,6 +709,9 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     tab.hlo = a.hist + (size_t)b * a.hist_rows * a.hist_w;
     tab.hhi = tab.hlo + (size_t)a.hist_rows * a.hist_w;
   }
+  if (SLIM)
+    slim_ops(tab, opw, kops, p.sd_reg != 0, xrow, s_xi, smem + (o.s_zero - o.s_at), p.Dm, lane,
+             so);
   if (!SLIM) {
 #pragma unroll
     for (int k = 0; k < OPS_REG; ++k) {
@@ -721,9 +740,9 @@ __device__ __forceinline__ void cons_rows(const RowsArgs& a, int hist_row0, int 
     double* hc = (hrow && a.hist_w > 3) ? hrow + 3 : nullptr;
     double f3;
     if constexpr (SLIM)
-      f3 = constraints_regs<FULL, true>(tab, opw, kops, srow, lane, grow, hc);
+      f3 = constraints_slim(tab, so, srow, lane, grow, hc);
     else
-      f3 = constraints_regs<FULL, false>(tab, opw, kops, (const double*)xrow, lane, grow, hc);
+      f3 = constraints_regs<FULL>(tab, opw, kops, (const double*)xrow, lane, grow, hc);
     // The row's destination is read from lane k HERE, with every lane active: a readlane
     // of a lane that is inactive at that point returns an undefined value.  (Round 3 read
     // it inside the lane-0 branch below.  Whenever the compiler spilled dst_v, its reload

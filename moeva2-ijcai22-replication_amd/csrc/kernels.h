@@ -31,7 +31,7 @@ __host__ __device__ inline size_t mlp_lds_bytes(int Dm4, int hmax, int Klast, in
 //                    -1, fixed) and fidx [V] (stored gene -> gene)        -> k_gen
 //                 C: ML scaler at the mutable features (mlS, mlM)         -> k_gen
 //                 S: the slim program of k_genc's phase 2 (DIFF / RATIO_SAFE lane ops and
-//                    ABS_SUMDIFF only): k (fp64), col, pool, sum-diff args -> LDS; the
+//                    ABS_SUMDIFF only): k (fp64), col, pool, sum-diff args, 0.0 -> LDS; the
 //                    ops' packed words (code | a0 << 4 | a1 << 18) read from HBM
 //   state blob    X: x_init                                               -> k_cons (k_gen OHE)
 //                 E: encoder MinMax at the mutable features (es, em, x0)  -> k_gen
@@ -39,7 +39,7 @@ struct VaryOff {
   unsigned opa, opk, opc, ocol, pool, a_end;      // region A at 0
   unsigned geo, ginfo, mutf, ooff, ofeat, cmap, fidx, b_at, b_end;  // region B at b_at
   unsigned mlS, mlM, c_at, c_end;                 // region C at c_at
-  unsigned s_k, s_col, s_pool, s_sd, s_at, s_end;  // region S (staged part) at s_at
+  unsigned s_k, s_col, s_pool, s_sd, s_zero, s_at, s_end;  // region S (staged part) at s_at
   unsigned s_opw, vb;                             // S packed op words; vb = blob bytes
   unsigned xi, x_end;                             // region X at 0
   unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
@@ -83,6 +83,7 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   o.s_col = take(C * 4);
   o.s_pool = take((size_t)p.n_pool * 4);
   o.s_sd = take((size_t)(p.n_sumdiff > 0 ? p.n_sumdiff : 1) * 16);
+  o.s_zero = take(16);  // a 0.0 (constraints_slim's absent sum-diff terms read it)
   o.s_end = kb(off);
   off = o.s_end;
   o.s_opw = take(C * 4);

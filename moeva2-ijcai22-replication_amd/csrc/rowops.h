@@ -179,9 +179,8 @@ __device__ __forceinline__ unsigned pack_op(const OpTab& t, int c) {
   return (unsigned)t.code[c] | ((unsigned)ar.x << 4) | ((unsigned)ar.y << 18);
 }
 
-// SLIM: every lane op is DIFF / RATIO_SAFE and held in opw (DProblem.slim); k from t.k1;
-// operands are SlotRow slots.
-template <bool FULL, bool SLIM = false, class XR>
+// (The slim program has its own straight-line form, constraints_slim below.)
+template <bool FULL, class XR>
 __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigned* opw, int kops,
                                                    const XR& xrow, int lane, double* grow,
                                                    double* hcols) {
@@ -203,9 +202,7 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
       if (code == 1)
         v = va[k] - vb[k];
       else if (code == 2)
-        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - (SLIM ? t.k1[c] : t.k[c].x);
-      else if constexpr (SLIM)
-        v = __builtin_nan("");
+        v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k[c].x;
       else
         v = eval_op<FULL>(t, c, xrow);
       if (v <= t.tol) v = 0.0;
@@ -216,7 +213,6 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
       acc3 += g;
     }
   }
-  if constexpr (!SLIM)
   for (int c = lane + 64 * OPS_REG; c < t.n_lane; c += 64) {
     double v = eval_op<FULL>(t, c, xrow);
     if (v <= t.tol) v = 0.0;
@@ -236,6 +232,119 @@ __device__ __forceinline__ double constraints_regs(const OpTab& t, const unsigne
         *MV_PTR(hcols + MV_IDX(t.col[c], t.C, CK_CONS_COL), t.hlo, t.hhi, CK_AT_HIST2) = g;
     }
     sdsum += g;
+  }
+  return wave_sum(acc3) + sdsum;
+}
+
+// The slim program's operands as LDS byte addresses in registers (k_genc; DProblem.slim),
+// set up once per workgroup by slim_ops: lane op k of this lane reads oa[k] and ob[k] -- the
+// SlotRow slot's place in the wave's row buffer (row_at) or region X (xi_at) -- and an unused
+// op slot reads the 0.0 of region S (zero_at) twice, so its column value is 0 - 0 = 0 with no
+// validity test.  rbits: the lane's RATIO_SAFE ops (bit k); rg: the op groups k with any
+// RATIO_SAFE lane (wave-uniform: the others never enter the quotient branch).  sd_reg
+// (DProblem.sd_reg): lane l's term of either side of ABS_SUMDIFF op j in sdl / sdr, the zero
+// slot past a side's end.
+constexpr int SD_REG = 2;
+struct SlimOps {
+  unsigned oa[OPS_REG], ob[OPS_REG];
+  unsigned rbits;
+  int rg;
+  bool sd_reg;
+  unsigned sdl[SD_REG], sdr[SD_REG];
+};
+__device__ __forceinline__ void slim_ops(const OpTab& t, const unsigned* opw, int kops,
+                                         bool sd_reg, const void* row, const void* xi,
+                                         const void* zero, int dm, int lane, SlimOps& so) {
+  const unsigned row_at = lds_addr(row), xi_at = lds_addr(xi), zero_at = lds_addr(zero);
+  auto slot_at = [&](int s) { return s < dm ? row_at + 8u * s : xi_at + 8u * (s - dm); };
+  so.rbits = 0;
+  so.rg = 0;
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    const unsigned w = opw[k];
+    const bool live = k < kops && lane + 64 * k < t.n_lane;
+    so.oa[k] = live ? slot_at((w >> 4) & 0x3FFF) : zero_at;
+    so.ob[k] = live ? slot_at(w >> 18) : zero_at;
+    const bool ratio = live && (w & 15) == 2;
+    so.rbits |= ratio ? 1u << k : 0u;
+    so.rg |= __ballot(ratio) ? 1 << k : 0;
+  }
+  so.sd_reg = sd_reg;
+  auto at = [&](int q, int end) { return q < end ? slot_at(t.pool[q]) : zero_at; };
+#pragma unroll
+  for (int j = 0; j < SD_REG; ++j) {
+    so.sdl[j] = zero_at;
+    so.sdr[j] = zero_at;
+    if (sd_reg && j < t.C - t.n_lane) {
+      const int4 ar = t.sd[j];
+      so.sdl[j] = at(ar.x + lane, ar.y);
+      so.sdr[j] = at(ar.y + lane, ar.z);
+    }
+  }
+}
+
+// constraints_regs for the slim program (every lane op DIFF or RATIO_SAFE, tol >= 0),
+// straight-line: every lane takes its op's difference, the RATIO_SAFE lanes of a group in rg
+// replace it with the quotient, and the clamp is  g = v <= tol ? 0 : v  -- the value of
+// constraints_regs's (v <= tol -> 0; v * (v > 0)) once tol >= 0: a v above tol is positive.
+// The unused slots' g = 0 leave the column sum bit-identical (it is never -0).  sd_reg:
+// (0 + l) - r  with the zero slot for an absent term is bit-identical to sumdiff_wave's
+// conditional += / -= (s - +0 == s); otherwise sumdiff_wave on the SlotRow view.
+template <class XR>
+__device__ __forceinline__ double constraints_slim(const OpTab& t, const SlimOps& so,
+                                                   const XR& xrow, int lane, double* grow,
+                                                   double* hcols) {
+  double va[OPS_REG], vb[OPS_REG];
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    va[k] = lds_ld(so.oa[k]);
+    vb[k] = lds_ld(so.ob[k]);
+  }
+  const double tol = t.tol;
+  double acc3 = 0.0;
+  // the columns' stores (G, history) in their own copy of the loop: a per-op store test
+  // kept a lane mask per op live across the row loop
+  auto lane_ops = [&](auto st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < OPS_REG; ++k) {
+      const int c = lane + 64 * k;
+      double v = va[k] - vb[k];
+      if ((so.rg >> k) & 1)
+        if ((so.rbits >> k) & 1) v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k1[c];
+      const double g = v <= tol ? 0.0 : v;
+      if (decltype(st)::value && c < t.n_lane) {
+        const int col = MV_IDX(t.col[c], t.C, CK_CONS_COL);
+        if (grow) grow[col] = g;
+        if (hcols) *MV_PTR(hcols + col, t.hlo, t.hhi, CK_AT_HIST2) = g;
+      }
+      acc3 += g;
+    }
+  };
+  if (grow || hcols)
+    lane_ops(std::true_type{});
+  else
+    lane_ops(std::false_type{});
+  double sdsum = 0.0;  // ABS_SUMDIFF columns (wave-uniform values)
+  auto sd_col = [&](int c, double v) {
+    const double g = v <= tol ? 0.0 : v;
+    if (lane == 0) {
+      if (grow) grow[t.col[c]] = g;
+      if (hcols) *MV_PTR(hcols + MV_IDX(t.col[c], t.C, CK_CONS_COL), t.hlo, t.hhi, CK_AT_HIST2) = g;
+    }
+    sdsum += g;
+  };
+  const int nsd = t.C - t.n_lane;
+  if (so.sd_reg) {
+#pragma unroll
+    for (int j = 0; j < SD_REG; ++j) {
+      if (j < nsd) {
+        const double l = lds_ld(so.sdl[j]);
+        const double r = lds_ld(so.sdr[j]);
+        sd_col(t.n_lane + j, fabs(wave_sum((0.0 + l) - r)));
+      }
+    }
+  } else {
+    for (int c = t.n_lane; c < t.C; ++c) sd_col(c, sumdiff_wave(t, c, xrow, lane));
   }
   return wave_sum(acc3) + sdsum;
 }
@@ -673,8 +782,9 @@ __device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, 
 }
 
 // The cached mutations of row k (position / value q held by lane 4 k + q, row_draws): each
-// position is wave-uniform, so its register index t = pos / 64 is a scalar branch and only
-// that register is updated, on lane pos % 64.
+// position is wave-uniform, so register t = pos / 64 takes the value on lane pos % 64 through
+// a lane-mask select on every register (a scalar branch on t made the compiler select a
+// pointer into x, which kept the caller's row buffers in scratch, or copy every register).
 template <int NT, int CAP>
 __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, int mposv, double mvalv,
                                                     int k, int lane) {
@@ -685,10 +795,9 @@ __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, int mpo
       const int pos = MV_IDX(pr, 64 * NT, CK_GEN_APPLY);
       const double y = rdl_d(mvalv, CAP * k + q);
       const int tt = pos >> 6;
-      const bool me = lane == (pos & 63);
+      const unsigned long long m = 1ull << (pos & 63);
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (t == tt) x[t] = me ? y : x[t];
+      for (int t = 0; t < NT; ++t) x[t] = select_lanes_d(x[t], y, t == tt ? m : 0ull);
     }
   }
 }

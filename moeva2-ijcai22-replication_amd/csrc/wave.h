@@ -128,6 +128,25 @@ __device__ __forceinline__ double wave_max(double v) {
   return nanmax(d0, d1);
 }
 
+// LDS byte addresses held in registers: lds_addr of a pointer into the kernel's LDS, and a
+// double loaded straight from such an address (one ds_read_b64 on the register -- a
+// generic base + offset made the compiler add the dynamic-LDS base, 0, to every address)
+typedef const __attribute__((address_space(3))) double lds_double;
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ double lds_ld(unsigned a) { return *(lds_double*)(uintptr_t)a; }
+
+// lanes set in the uniform mask m take b, the others a: one v_cndmask per half on the SGPR
+// pair (no branch, no EXEC change -- a select the compiler cannot turn into a switch over
+// register indices)
+__device__ __forceinline__ double select_lanes_d(double a, double b, unsigned long long m) {
+  unsigned lo, hi;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lo) : "v"(__double2loint(a)), "v"(__double2loint(b)), "s"(m));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(hi) : "v"(__double2hiint(a)), "v"(__double2hiint(b)), "s"(m));
+  return __hiloint2double((int)hi, (int)lo);
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
