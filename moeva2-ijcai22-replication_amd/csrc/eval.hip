@@ -391,9 +391,13 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
   const double* sgl = a.s.gl + (size_t)b * V;  // genetic bounds (SBX rows read all of them)
   const double* sgu = a.s.gu + (size_t)b * V;
   const bool sbx = SBX && a.mode == 1;
+  const PoolRsrc pool = pool_rsrc(gin, (size_t)a.in_rows * V);
+  unsigned pkey[NT];  // load_parent_row's crossover keys of this lane's genes
+#pragma unroll
+  for (int t = 0; t < NT; ++t) pkey[t] = parent_key(ginf[t]);
   auto load_row = [&](int k, double* x) {
     k = MV_IDX(k, min(nrw, 64), CK_GEN_LANE);
-    load_parent_row<NT>(gin, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), ginf, lane, x,
+    load_parent_row<NT>(pool, V, rdl(par_v, k), rdl(cx0_v, k), rdl(cx1_v, k), pkey, lane, x,
                         (long long)a.in_rows * V);
   };
   // Two rows' parent genes in flight ahead of the row being finished: under load an HBM
@@ -547,13 +551,16 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     }
   } else {
     // one row in flight, two row buffers taking turns (a rotation through a copy cost ten
-    // moves per row: the copy, and the loop-carried copy back)
+    // moves per row: the copy, and the loop-carried copy back).  The next row's loads are
+    // unconditional (the last row re-reads row nrw - 1, from L2): loads under a branch made
+    // the compiler's counter waits assume they might be missing, so every use of the current
+    // row waited for the next row's loads as well.
     double xc[NT];
     for (int k = 0; k < nrw; k += 2) {
-      if (k + 1 < nrw) load_row(k + 1, xc);
+      load_row(min(k + 1, nrw - 1), xc);
       do_row(k, xa);
       if (k + 1 >= nrw) break;
-      if (k + 2 < nrw) load_row(k + 2, xa);
+      load_row(min(k + 2, nrw - 1), xa);
       do_row(k + 1, xc);
     }
   }

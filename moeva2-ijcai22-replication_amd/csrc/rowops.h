@@ -754,30 +754,51 @@ __device__ __forceinline__ void mlp2_layer(const float* __restrict__ A, int lda,
   }
 }
 
-// Parent genes of one child row (k_gen, k_rows / the whole-attack row phase): lane l loads
-// genes l + 64 t from the own or the other parent.  32-bit element offsets from the state's
-// pool (S * V < 2^31) with the two parents' row offsets wave-uniform, and swapped_packed in
-// branch-free form: the segment [lo, lo + n) of each subset (n = 0 when the subset's
-// crossover is off) as scalars, one unsigned compare per gene.  (64-bit pointer arithmetic
-// and the branchy test per gene were about a third of k_gen's row-loop VALU.)
+// Parent genes of one child row (k_gen / k_genc): lane l loads genes l + 64 t from the own or
+// the other parent through a buffer resource over the state's pool: the byte offset is the
+// chosen parent's row offset plus 8 l (one select per gene between two per-row values), and
+// 512 t rides in the load's immediate offset.  Genes past V (the last register's padding
+// lanes, never stored) may read past the row; past the pool the buffer's range check returns
+// 0 instead of faulting.  Crossover test per gene: pkey = the gene's position in its subset,
+// + 0x10000 in the second (integer) subset, so an unsigned compare against each subset's
+// segment [lo, lo + n) -- n = 0 when the subset's crossover is off -- decides it with no
+// per-gene selects (a gene of one subset is never inside the other's shifted segment).
+struct PoolRsrc {
+  __amdgpu_buffer_rsrc_t r;
+};
+__device__ __forceinline__ PoolRsrc pool_rsrc(const double* base, size_t elems) {
+  const size_t bytes = elems * 8;
+  return PoolRsrc{__builtin_amdgcn_make_buffer_rsrc(
+      (void*)base, (short)0, (int)(bytes < 0x7FFFFFFFull ? bytes : 0x7FFFFFFFull), 0x00020000)};
+}
+__device__ __forceinline__ unsigned parent_key(int ginf) {
+  return (unsigned)((ginf >> 2) & 0x7FFF) + ((ginf & 3) == 0 ? 0u : 0x10000u);
+}
 template <int NT>
-__device__ __forceinline__ void load_parent_row(const double* __restrict__ gin, int V, int pr,
-                                                int cx0, int cx1, const int (&ginf)[NT],
-                                                int lane, double* x, long long pool_elems = 0) {
-  int Vo = V;
-  asm volatile("" : "+s"(Vo));  // keep the per-t bounds out of loop-invariant hoisting
-  const unsigned own = (unsigned)(pr & 0xFFFF) * (unsigned)Vo;
-  const unsigned oth = (unsigned)(pr >> 16) * (unsigned)Vo;
-  const int lo0 = (cx0 >> 1) & 0x7FFF, lo1 = (cx1 >> 1) & 0x7FFF;
-  const unsigned n0 = (cx0 & 1) ? (unsigned)((cx0 >> 16) - lo0) : 0u;
-  const unsigned n1 = (cx1 & 1) ? (unsigned)((cx1 >> 16) - lo1) : 0u;
+__device__ __forceinline__ void load_parent_row(const PoolRsrc& pool, int V, int pr, int cx0,
+                                                int cx1, const unsigned (&pkey)[NT], int lane,
+                                                double* x, long long pool_elems = 0) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  unsigned own8 = (unsigned)(pr & 0xFFFF) * (unsigned)V * 8u;
+  unsigned oth8 = (unsigned)(pr >> 16) * (unsigned)V * 8u;
+  // opaque, so the compiler selects these two offsets instead of the two row indices (which
+  // it then multiplied per gene: a quarter-rate v_mul_lo_u32 each)
+  asm("" : "+s"(own8), "+s"(oth8));
+  own8 += 8u * (unsigned)lane;
+  oth8 += 8u * (unsigned)lane;
+  asm("" : "+v"(own8), "+v"(oth8));  // and 512 t stays the loads' immediate offset
+  const int s0 = (cx0 >> 1) & 0x7FFF, s1 = (cx1 >> 1) & 0x7FFF;
+  const unsigned lo0 = (unsigned)s0, lo1 = (unsigned)s1 + 0x10000u;
+  const unsigned n0 = (cx0 & 1) ? (unsigned)((cx0 >> 16) - s0) : 0u;
+  const unsigned n1 = (cx1 & 1) ? (unsigned)((cx1 >> 16) - s1) : 0u;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
-    const int g = lane + 64 * t;
-    const unsigned gc = (unsigned)(g < Vo ? g : Vo - 1);
-    const bool real = (ginf[t] & 3) == 0;
-    const unsigned d = (unsigned)(((ginf[t] >> 2) & 0x7FFF) - (real ? lo0 : lo1));
-    x[t] = gin[MV_IDX((d < (real ? n0 : n1) ? oth : own) + gc, pool_elems, CK_AT_PARENT)];
+    const bool cross = pkey[t] - lo0 < n0 || pkey[t] - lo1 < n1;
+    const unsigned off = cross ? oth8 : own8;
+    if (MV_CHECKS_ON && lane + 64 * t < V)
+      (void)MV_IDX((long long)(off / 8 + 64 * t), pool_elems, CK_AT_PARENT);
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(pool.r, off + 512u * t, 0, 0);
+    x[t] = __hiloint2double((int)w.y, (int)w.x);
   }
 }
 
