@@ -368,7 +368,7 @@ def run_workload(name, w, args, device, world, rank, steps, warmup, bf16, crosso
     # xml_direct (mv_get_mlp_kernel = 1: IDENT problems whose classifier is k_mlp2 reading
     # the genes): k_gen writes no fp32 ML row, k_mlp2 reads the child genes itself
     prog = eng.prog
-    xml_direct = kt["mlp_kernel"] == "k_mlp2(genes)"
+    xml_direct = kt["mlp_kernel"] in ("k_mlp2(genes)", "k_mlpr(genes)")
     gen_bytes = 2 * V * 8 + (0 if xml_direct else Dm4 * 4) + 8
     cons_bytes = V * 8 + 8
     surv_bytes_state = (P + O) * 3 * 8 + 4 * (P + 2 * O)

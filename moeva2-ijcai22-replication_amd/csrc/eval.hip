@@ -1522,6 +1522,354 @@ __global__ __launch_bounds__(256, BF ? (CJ == 1 ? 3 : 2) : (DIRECT && CJ == 1 ? 
 }
 
 // ---------------------------------------------------------------------------------------
+// k_mlpr: the fp32 classifier of the gene-reading (xml_direct) path for hidden widths up to
+// 64 -- the botnet headline's 312-64-64-32-2 chain -- with every wave on its own RW x 16 rows
+// and no LDS tile, no barrier in the row loop.  Each Dense layer runs transposed,
+// out^T = W^T . in^T, on v_mfma_f32_16x16x4f32: the weights are the A operand (lane (il, ka)
+// = output column 16 nb + il, k = 16 kg + 4 ka + s: one dwordx4 of the packed Wp per k-group
+// and column block, from L2), the rows the B operand (lane (il, ka) = row il, the same k), so
+// column block nb's accumulator holds outputs 16 nb + 4 ka + j of row il -- exactly the next
+// layer's B operand for k-group nb: the hidden layers never leave the registers.  Layer 0's B
+// operands are the row's genes scaled as k_gen would, (float)(x * mlS + mlM), 32 B per lane
+// per k-group from HBM, one k-group ahead in two alternating operand sets.  Every output sums
+// the same products in the same k order as k_mlp2 (k-group, then s; the MFMA's k slot is ka
+// either way) and the last Dense keeps k_mlp2's four-quarter order, so f1 is bit-identical
+// (oracle/device_order.f1_device_order).  Replaces k_mlp2's 64-row tiles, whose layer-0 chunk
+// loop waited on its LDS staging (~64 k cycles per tile against ~14 k of MFMA issue).
+#ifndef MV_MLPR_OCC
+#define MV_MLPR_OCC 3  // waves per SIMD of the 16-row instance (<= 168 registers)
+#endif
+// LDS: the ML scaler at the mutable features (mlS, mlM), the final Dense layer, the hidden
+// layers' packed weights and biases (read per tile: from L2 each hidden layer waited out a
+// ~3 k-cycle round trip, MV_MLP_PHASES "hidden" 16.9 k cycles per tile), then per wave its
+// tile's bias1 rows (landed by LDS DMA while layer 0 runs) and its last-hidden-layer rows.
+struct MlprLds {
+  unsigned wl, hw, hb, b1, hs, wst, total;
+  int hld;  // fp32 row stride of a wave's last-hidden-layer rows
+};
+__host__ __device__ inline MlprLds mlpr_lds(const DProblem& p, int rw) {
+  const int nl = p.n_layers;
+  MlprLds L{};
+  L.wl = (unsigned)p.Dm4 * 16;  // mlS, mlM
+  L.hld = p.dims[nl - 1] + 4;
+  L.hw = L.wl + (((unsigned)(p.dims[nl - 1] * p.dims[nl] + p.dims[nl]) * 4 + 15) & ~15u);
+  unsigned w = 0, b = 0;
+  for (int l = 1; l + 1 < nl; ++l) {
+    w += (unsigned)(p.dims[l] * p.dims[l + 1]);
+    b += (unsigned)p.dims[l + 1];
+  }
+  L.hb = L.hw + w * 4;
+  // a wave's bias1 rows are in registers before its last-hidden-layer rows are written: one
+  // per-wave region serves both
+  L.b1 = L.hb + ((b * 4 + 15) & ~15u);
+  L.hs = L.b1;
+  L.wst = (unsigned)rw * 4 * 1024;
+  const unsigned hsz = (unsigned)(rw * 16 * L.hld) * 4;
+  L.wst = L.wst > hsz ? L.wst : hsz;
+  L.total = L.b1 + 4u * L.wst;
+  return L;
+}
+// The shapes k_mlpr takes: IDENT gene rows (xml_direct) of an even gene count (16-B aligned
+// gene pairs), fp32, every MFMA layer's width a multiple of 16 and at most 64, K0 a multiple
+// of 16, at most 8 classes.
+__host__ __device__ inline bool mlpr_ok(const DProblem& p) {
+  if (!p.xml_direct || p.mlp_bf16 || !p.mlp2 || p.n_layers < 2 || (p.Dm & 1) || p.Dm < 2)
+    return false;
+  for (int l = 0; l + 1 < p.n_layers; ++l)
+    if (!p.Wp[l]) return false;
+  for (int l = 1; l < p.n_layers; ++l)
+    if (p.dims[l] % 16 || p.dims[l] > 64) return false;
+  return p.Dm4 % 16 == 0 && p.dims[p.n_layers] <= 8 && mlpr_lds(p, 2).total <= 96 * 1024;
+}
+
+template <int RW, int NO>
+__global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slot, int hist_row0) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowsArgs& a = c_rows[slot];
+  const DProblem& p = a.p;
+  constexpr int TR = 16 * RW;  // rows per wave tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int il = lane & 15, ka = lane >> 4;
+  const int nl = p.n_layers;
+  const int K0 = p.Dm4, N0 = p.dims[1], Dm = p.Dm;
+  const int Klast = p.dims[nl - 1], nout = p.dims[nl];
+  const MlprLds L = mlpr_lds(p, RW);
+  const int hld = L.hld;
+  double* sS = (double*)smem;
+  double* sM = sS + K0;
+  float* wl = (float*)(smem + L.wl);
+  float* bl = wl + Klast * nout;
+  float* hs = (float*)(smem + L.hs + wave * L.wst);
+  for (int q = tid; q < K0; q += 256) {
+    sS[q] = p.mlS[q];
+    sM[q] = p.mlM[q];
+  }
+  for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
+  if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
+  float* hw = (float*)(smem + L.hw);
+  float* hbs = (float*)(smem + L.hb);
+  for (int l = 1, wo = 0, bo = 0; l + 1 < nl; wo += p.dims[l] * p.dims[l + 1], bo += p.dims[l + 1], ++l) {
+    for (int q = tid; q < (p.dims[l] * p.dims[l + 1]) >> 2; q += 256)
+      *(float4*)(hw + wo + 4 * q) = *(const float4*)(p.Wp[l] + 4 * q);
+    for (int q = tid; q < p.dims[l + 1]; q += 256) hbs[bo + q] = p.bias[l][q];
+  }
+  unsigned char* b1w = smem + L.b1 + wave * L.wst;
+  __syncthreads();
+  const int ntiles = (a.total + TR - 1) / TR;
+  const int nkg0 = K0 >> 4, nb0 = N0 >> 4;
+  const float* Wp0 = p.Wp[0];
+  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {
+    const int r0 = tile * TR;
+    // development phase clocks (MV_CLOCKS build, MV_MLP_PHASES=1): wave 0's first tile
+    const bool ph = MV_CLOCKS && a.mphase && tid == 0 && tile == (int)blockIdx.x * 4;
+    long long* phq = a.mphase + (size_t)blockIdx.x * 16;
+    if (ph) {
+      phq[0] = clock64();
+      phq[6] = wall_clock64();
+    }
+    const double* grow[RW];
+    int rst[RW];
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt) {
+      const int rr0 = r0 + 16 * rt + il;
+      const int rr = rr0 < a.total ? rr0 : a.total - 1;
+      const int st = rr / a.n, i = rr - st * a.n;
+      rst[rt] = st;
+      grow[rt] = a.mode == 1
+          ? a.genes_out + ((size_t)st * a.out_rows +
+                           MV_IDX(a.out_map ? a.out_map[rr] : i, a.out_rows, CK_MLP_ROW)) * Dm
+          : a.genes_in + ((size_t)st * a.in_rows + MV_IDX(i, a.in_rows, CK_MLP_ROW)) * Dm;
+    }
+    // the epilogue's per-state bias1 rows (immutable features folded) by LDS DMA: lane l's
+    // 16 B of block (rt, nb) land at b1w + (4 rt + nb) KiB + 16 l; the oldest loads of the
+    // tile, so layer 0's waits retire them
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int nbc = nb < nb0 ? nb : nb0 - 1;
+        __builtin_amdgcn_global_load_lds(a.s.bias1 + (size_t)rst[rt] * N0 + 16 * nbc + 4 * ka,
+                                         b1w + (4 * rt + nb) * 1024, 16, 0, 0);
+      }
+    floatx4 acc[RW][4];
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[rt][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // operands: the four column blocks' weights in two alternating sets (L2 hits, one k-group
+    // ahead), the RW rows' four genes in a ring of four sets (HBM, three k-groups ahead: with
+    // one k-group in flight per wave the launch ran at the latency of a round trip per
+    // k-group, ~2.5 us, MV_MLPR A/B v1).  Each step issues the next weights BEFORE its genes:
+    // vmcnt retires in order, so waiting for weights issued after the genes of later steps
+    // would wait for those genes too.
+    float4 wA[4], wB[4];
+    double2 g0[RW][2], g1[RW][2], g2[RW][2], g3[RW][2];
+#define MR_LOADW(kg, w)                                                                    \
+  {                                                                                        \
+    const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
+    _Pragma("unroll") for (int nb = 0; nb < 4; ++nb) {                                     \
+      const int nbc = nb < nb0 ? nb : nb0 - 1;                                             \
+      w[nb] = *(const float4*)(Wp0 + ((size_t)kgc * N0 + nbc * 16 + il) * 16 + 4 * ka);    \
+    }                                                                                      \
+  }
+#define MR_LOADG(kg, g)                                                                    \
+  {                                                                                        \
+    const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
+    const int k = 16 * kgc + 4 * ka;                                                       \
+    const int k01 = k + 1 < Dm ? k : Dm - 2, k23 = k + 3 < Dm ? k + 2 : Dm - 2;            \
+    _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                    \
+      g[rt][0] = *(const double2*)(grow[rt] + k01);                                        \
+      g[rt][1] = *(const double2*)(grow[rt] + k23);                                        \
+    }                                                                                      \
+  }
+#define MR_STEP(kg, w, g)                                                                  \
+  {                                                                                        \
+    const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
+    const int k = 16 * kgc + 4 * ka;                                                       \
+    const double2 s01 = *(const double2*)(sS + k), s23 = *(const double2*)(sS + k + 2);    \
+    const double2 m01 = *(const double2*)(sM + k), m23 = *(const double2*)(sM + k + 2);    \
+    const double sc[4] = {s01.x, s01.y, s23.x, s23.y}, mn[4] = {m01.x, m01.y, m23.x, m23.y}; \
+    /* k >= Dm (the zero padding to K0) and the k-groups past nkg0: +0 */                  \
+    unsigned msk[4];                                                                       \
+    _Pragma("unroll") for (int e = 0; e < 4; ++e)                                          \
+      msk[e] = (k + e < Dm && (kg) < nkg0) ? 0xFFFFFFFFu : 0u;                             \
+    float xb[RW][4];                                                                       \
+    _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                    \
+      const double gv[4] = {g[rt][0].x, g[rt][0].y, g[rt][1].x, g[rt][1].y};               \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e)                                        \
+        xb[rt][e] = __uint_as_float(__float_as_uint((float)(gv[e] * sc[e] + mn[e])) & msk[e]); \
+    }                                                                                      \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s)                                          \
+      _Pragma("unroll") for (int nb = 0; nb < 4; ++nb)                                     \
+        _Pragma("unroll") for (int rt = 0; rt < RW; ++rt)                                  \
+          acc[rt][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(w[nb], s), xb[rt][s],     \
+                                                             acc[rt][nb], 0, 0, 0);        \
+  }
+    // the empty asm statements with a memory clobber keep each prefetch where it is written:
+    // without them instcombine folds phi(load, load) into one load at the loop top and the
+    // scheduler sinks every load next to its first use (vmcnt(0) before each MFMA group)
+    const int nkg0e = (nkg0 + 3) & ~3;
+    MR_LOADW(0, wA)
+    MR_LOADG(0, g0)
+    MR_LOADG(1, g1)
+    MR_LOADG(2, g2)
+    if (ph) phq[1] = clock64();
+#pragma unroll 1
+    for (int kg = 0; kg < nkg0e; kg += 4) {
+      MR_LOADW(kg + 1, wB)
+      MR_LOADG(kg + 3, g3)
+      asm volatile("" ::: "memory");
+      MR_STEP(kg, wA, g0)
+      MR_LOADW(kg + 2, wA)
+      MR_LOADG(kg + 4, g0)
+      asm volatile("" ::: "memory");
+      MR_STEP(kg + 1, wB, g1)
+      MR_LOADW(kg + 3, wB)
+      MR_LOADG(kg + 5, g1)
+      asm volatile("" ::: "memory");
+      MR_STEP(kg + 2, wA, g2)
+      MR_LOADW(kg + 4, wA)
+      MR_LOADG(kg + 6, g2)
+      asm volatile("" ::: "memory");
+      MR_STEP(kg + 3, wB, g3)
+      if (ph && kg == 0) phq[2] = clock64();
+    }
+    if (ph) phq[3] = clock64();
+    // bias1 landed (its DMA is older than every layer-0 load still in flight)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float4 b1v[RW][4];
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        b1v[rt][nb] = *(const float4*)(b1w + (4 * rt + nb) * 1024 + 16 * lane);
+#undef MR_LOADW
+#undef MR_LOADG
+#undef MR_STEP
+    // layer-0 epilogue: + bias1, ReLU
+    floatx4 h[RW][4];
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const float4 b = b1v[rt][nb];
+        const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[rt][nb][j] + bv[j];
+          h[rt][nb][j] = v > 0.f && nb < nb0 ? v : 0.f;  // blocks past N0 feed +0
+        }
+      }
+    // hidden layers: the previous layer's column block kg is this layer's k-group kg
+    const float* Wl = hw;
+    const float* bh = hbs;
+#pragma unroll 1
+    for (int l = 1; l + 1 < nl; Wl += p.dims[l] * p.dims[l + 1], bh += p.dims[l + 1], ++l) {
+      const int N = p.dims[l + 1], nkg = p.dims[l] >> 4, nbo = N >> 4;
+#pragma unroll
+      for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) acc[rt][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // every k-group and column block runs: the previous layer's blocks past its width
+      // are +0 (adding +0 products leaves each sum's bits unchanged), and this layer's blocks
+      // past N are computed on clamped weights and zeroed below
+#pragma unroll
+      for (int kg = 0; kg < 4; ++kg) {
+        float4 w[4];
+        const int kgc = kg < nkg ? kg : nkg - 1;
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          const int nbc = nb < nbo ? nb : nbo - 1;
+          w[nb] = *(const float4*)(Wl + ((size_t)kgc * N + nbc * 16 + il) * 16 + 4 * ka);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+            for (int rt = 0; rt < RW; ++rt)
+              acc[rt][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(w[nb], s), h[rt][kg][s],
+                                                                 acc[rt][nb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int nbc = nb < nbo ? nb : nbo - 1;
+        const float4 b = *(const float4*)(bh + 16 * nbc + 4 * ka);
+        const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float v = acc[rt][nb][j] + bv[j];
+            h[rt][nb][j] = v > 0.f && nb < nbo ? v : 0.f;
+          }
+      }
+    }
+    if (ph) phq[4] = clock64();
+    // final Dense + softmax (classifier.py:23-29) -> f1, k_mlp2's order: quarter w of the
+    // last hidden layer's Klast inputs as one fmaf chain from 0, then ((q0 + q1) + q2) + q3
+    // + bias.  The wave's rows go through its LDS rows; lane (row, qh) sums RW quarters.
+#pragma unroll
+    for (int rt = 0; rt < RW; ++rt)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        if (nb < (Klast >> 4))
+          *(float4*)(hs + (16 * rt + il) * hld + 16 * nb + 4 * ka) =
+              make_float4(h[rt][nb][0], h[rt][nb][1], h[rt][nb][2], h[rt][nb][3]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int row = lane % TR, qh = lane / TR;
+    const int kq = Klast >> 2;
+    float ps[RW][NO];
+#pragma unroll
+    for (int qi = 0; qi < RW; ++qi) {
+      const int k0 = (qh * RW + qi) * kq;
+      const float* ir = hs + row * hld + k0;
+      const float* wq = wl + k0 * nout;
+#pragma unroll
+      for (int c = 0; c < NO; ++c) ps[qi][c] = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < kq; ++k) {
+        const float v = ir[k];
+#pragma unroll
+        for (int c = 0; c < NO; ++c)
+          if (c < nout) ps[qi][c] = fmaf(v, wq[k * nout + c], ps[qi][c]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // hs is rewritten by the next tile
+    float q[4][NO];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int c = 0; c < NO; ++c) q[w][c] = __shfl(ps[w % RW][c], row + TR * (w / RW), 64);
+    const int rr0 = r0 + row;
+    if (qh == 0 && rr0 < a.total) {
+      const int s = rr0 / a.n, i = rr0 - s * a.n;
+      double z[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      double mx = -__builtin_inf();
+#pragma unroll
+      for (int c = 0; c < NO; ++c) {
+        if (c < nout) {
+          z[c] = (double)((((q[0][c] + q[1][c]) + q[2][c]) + q[3][c]) + bl[c]);
+          mx = z[c] > mx ? z[c] : mx;
+        }
+      }
+      const double f1 = softmax_pick(z, nout, mx, a.s.min_class[s]);
+      if (a.F) {
+        const int orow = MV_IDX(a.out_map ? a.out_map[rr0] : i, a.out_rows, CK_MLP_OUT);
+        a.F[((size_t)MV_IDX(s, a.total / a.n, CK_MLP_OUT) * a.out_rows + orow) * 3] = f1;
+      }
+      if (a.hist)
+        a.hist[((size_t)s * a.hist_rows + MV_IDX(hist_row0 + i, a.hist_rows, CK_MLP_OUT)) *
+               a.hist_w] = f1;
+    }
+    if (ph) {
+      phq[5] = clock64();
+      phq[7] = wall_clock64();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // k_mlpw: the bf16 perf mode for WIDE hidden layers (BASELINE configs[4]: 756-512-512-256-2,
 // widths up to 512) -- 64-row persistent tiles, 8 waves.  Activations live in LDS as bf16
 // (two [64][hs] ping-pong buffers, 133 KiB at width 512; fp32 tiles of 64 rows would not
@@ -2471,6 +2819,37 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
                         : mlp2_go3<CJ, BF, false, false>(a, slot, hist_row0, stream);
 }
 
+template <int RW, int NO>
+static hipError_t mlpr_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
+  static size_t occ_lds = 0;
+  static int occ = 1;
+  const size_t lds = mlpr_lds(a.p, RW).total;
+  if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlpr<RW, NO>, 256, lds) != hipSuccess ||
+        n < 1)
+      n = 1;
+    (void)hipGetLastError();
+    occ = n;
+    occ_lds = lds;
+  }
+  const int ntiles = (a.total + 16 * RW - 1) / (16 * RW);
+  const int need = (ntiles + 3) / 4;
+  const int grid = need < occ * cu_count() ? need : occ * cu_count();
+  hipLaunchKernelGGL((k_mlpr<RW, NO>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
+  return hipGetLastError();
+}
+
+// k_mlpr's rows per wave tile: MV_MLPR_RW=1 (16) or 2 (32, default)
+static bool use_mlpr(const DProblem& p) {
+  static const bool off = std::getenv("MV_MLPR") && std::getenv("MV_MLPR")[0] == '0';
+  return !off && mlpr_ok(p);
+}
+static int mlpr_rw() {
+  static const int rw = std::getenv("MV_MLPR_RW") ? std::atoi(std::getenv("MV_MLPR_RW")) : 1;
+  return rw == 1 ? 1 : 2;
+}
+
 template <int CJ>
 static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static bool configured = false;
@@ -2508,9 +2887,10 @@ static bool use_mlpw32(const DProblem& p) {
 
 // launch_mlp's choice for a problem: 0 k_mlp, 1 k_mlp2 reading the genes (xml_direct),
 // 2 k_mlp2 reading the fp32 ML rows, 4 k_mlpw (bf16), 5 k_mlpw32 (fp32 wide), -1 no model
-// (3, k_mlp2x, was retired)
+// (3, k_mlp2x, was retired), 6 k_mlpr (gene-reading, hidden widths <= 64)
 int mlp_kernel_kind(const DProblem& p) {
   if (p.n_layers == 0) return -1;
+  if (use_mlpr(p)) return 6;
   if (p.mlp2 && !std::getenv("MV_MLP_V1") && !(p.mlp_bf16 && std::getenv("MV_MLPW")))
     return p.xml_direct ? 1 : 2;
   if (p.mlp_bf16 && mlpw_lds(p).total <= 160 * 1024 && !std::getenv("MV_MLPW_OFF")) return 4;
@@ -2520,6 +2900,13 @@ int mlp_kernel_kind(const DProblem& p) {
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
+  if (use_mlpr(a.p)) {
+    if (a.p.dims[a.p.n_layers] <= 2)
+      return mlpr_rw() == 1 ? mlpr_go<1, 2>(a, slot, hist_row0, stream)
+                            : mlpr_go<2, 2>(a, slot, hist_row0, stream);
+    return mlpr_rw() == 1 ? mlpr_go<1, 8>(a, slot, hist_row0, stream)
+                          : mlpr_go<2, 8>(a, slot, hist_row0, stream);
+  }
   // (MV_MLPW=1: the bf16 mode runs k_mlpw for narrow nets too -- development A/B)
   if (a.p.mlp2 && !std::getenv("MV_MLP_V1") && !(a.p.mlp_bf16 && std::getenv("MV_MLPW"))) {
     if (a.p.mlp_bf16)

@@ -138,6 +138,63 @@ def test_evaluate_bit_exact_in_engine_order(name):
             np.testing.assert_allclose(F[b, :, 2], ref[:, 2], rtol=1e-14, atol=0)
 
 
+@pytest.mark.parametrize("dims", [(756, 48, 32, 16, 3), (756, 64, 2), (756, 32, 64, 48, 2)])
+def test_row_classifier_shapes_bit_exact(dims):
+    """k_mlpr (the gene-reading fp32 classifier: each wave on its own 32 rows, the Dense layers
+    transposed on MFMA, hidden layers in registers) on shapes other than the shipped botnet
+    net -- widths below 64 (column blocks past a layer's width zeroed), one hidden layer,
+    three classes: mv_evaluate's F (full gene layout, mode 0) and a short attack's final F
+    (compact layout, offspring rows through out_map) bit-identical to oracle/device_order,
+    i.e. to k_mlp2's summation order."""
+    import dataclasses
+
+    from oracle import device_order as do
+    from moeva2_amd.attacks.moeva2.classifier import Classifier, DenseMLPModel
+    from moeva2_amd.attacks.moeva2.ref_dirs import energy_ref_dirs
+    from moeva2_amd.io.tf_bundle import DenseMLP
+    from moeva2_amd.problem import build_device_program, get_engine
+
+    p = Project("botnet")
+    W, _ = _wide_mlp(dims, seed=3)
+    rng = np.random.default_rng(4)
+    bs = [(0.1 * rng.standard_normal(b)).astype(np.float32) for b in dims[1:]]
+    clf = Classifier(DenseMLPModel(DenseMLP(W, bs, ["relu"] * (len(dims) - 2) + ["softmax"])))
+    c, sc = make_constraints("botnet"), make_scaler("botnet")
+    codes = build_device_program(c).op_code
+    eng = get_engine(c, clf, sc, 2)
+    X = p.x[:3]
+    bounds = [c.get_feature_min_max(dynamic_input=x) for x in X]
+    eng.set_states(X, np.array([b[0] for b in bounds]), np.array([b[1] for b in bounds]), 1)
+    assert eng.kernel_times()["mlp_kernel"] == "k_mlpr(genes)"
+    probs = [dataclasses.replace(p.problem(X[b]), weights=W, biases=bs) for b in range(3)]
+    n = 45
+    genes = np.empty((3, n, p.lay.V))
+    for b in range(3):
+        gl, gu = mo.genetic_bounds(p.lay, probs[b].xl, probs[b].xu)
+        g = np.repeat(mo.initial_population(probs[b], 1), n, axis=0)
+        for r in range(n):
+            k = rng.integers(0, p.lay.V, size=1 + r % 5)
+            g[r, k] = np.round(rng.uniform(gl[k], gu[k]))
+        genes[b] = g
+    F = torch.empty((3, n, 3), dtype=torch.float64, device="cuda")
+    eng.evaluate(torch.as_tensor(genes, device="cuda"), F)
+    F = F.cpu().numpy()
+    for b in range(3):
+        ref = do.evaluate_device_order(probs[b], genes[b], codes)
+        np.testing.assert_array_equal(F[b], ref)
+    eng.attack_run(4, 23, 10, 5, energy_ref_dirs(3, 20, 1), 0.05, 0)
+    ga = torch.empty((3, 23, p.lay.V), dtype=torch.float64, device="cuda")
+    Fa = torch.empty((3, 23, 3), dtype=torch.float64, device="cuda")
+    eng.attack_population(ga, Fa)
+    torch.cuda.synchronize()
+    fixed = np.zeros(p.lay.mutable_mask.shape[0], bool)
+    fixed[np.where(p.lay.mutable_mask)[0][~eng.stored_genes()]] = True
+    ga, Fa = ga.cpu().numpy(), Fa.cpu().numpy()
+    for b in range(3):
+        ref = do.evaluate_device_order(probs[b], ga[b], codes, fixed=fixed)
+        np.testing.assert_array_equal(Fa[b], ref)
+
+
 def _wide_mlp(dims=(756, 512, 512, 256, 2), seed=7):
     """bench.py's configs[4] classifier: Dense relu x3 + softmax, weights ~ N(0, 1/fan_in)."""
     rng = np.random.default_rng(seed)

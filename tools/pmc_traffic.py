@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_genc": "k_genc<", "k_narrow": "k_narrow<",
-        "k_mlp": "k_mlp2<", "k_survive": "k_survive<"}
+        "k_mlp": ("k_mlp2<", "k_mlpr<"), "k_survive": "k_survive<"}
 
 
 def per_dispatch(paths, counter):
@@ -28,7 +28,8 @@ def per_dispatch(paths, counter):
                 if r["Counter_Name"] != counter:
                     continue
                 for key, pat in KEYS.items():
-                    if pat in r["Kernel_Name"]:
+                    pats = pat if isinstance(pat, tuple) else (pat,)
+                    if any(q in r["Kernel_Name"] for q in pats):
                         tot[key][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: (sum(v.values()) / len(v), len(v)) for k, v in tot.items() if v}
 

@@ -13,12 +13,12 @@ import sys
 from collections import defaultdict
 
 KEYS = {"k_gen": "k_gen<", "k_cons": "k_cons<", "k_genc": "k_genc<", "k_narrow": "k_narrow<",
-        "k_mlp": "k_mlp2<", "k_mlp2x": "k_mlp2x<", "k_predict": "k_predict<", "k_survive": "k_survive<"}
+        "k_mlp": ("k_mlp2<", "k_mlpr<"), "k_mlp2x": "k_mlp2x<", "k_predict": "k_predict<", "k_survive": "k_survive<"}
 
 
 def key(name):
     for k, p in KEYS.items():
-        if p in name:
+        if any(q in name for q in (p if isinstance(p, tuple) else (p,))):
             return k
     return "other"
 
