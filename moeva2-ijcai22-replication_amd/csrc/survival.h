@@ -905,17 +905,25 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         double v = has ? L.red[lane * 16 + i] : __builtin_inf();
         int ix = has ? (int)L.red[lane * 16 + 3 + i] : INT_MAX;
         double w = has ? L.red[lane * 16 + 6 + i] : -__builtin_inf();
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          const double ov = __shfl_xor(v, off, 16);
-          const int oi = __shfl_xor(ix, off, 16);
-          const double ow = __shfl_xor(w, off, 16);
-          if (ov < v || (ov == v && oi < ix)) {
-            v = ov;
-            ix = oi;
-          }
-          w = max_prop(w, ow);
-        }
+        // within the 16-lane row by DPP (quad xor 1, xor 2, half mirror, mirror: every lane
+        // ends with the row's result, as in wave_reduce); ds_bpermute shuffles here cost
+        // ~6 k cycles per state (MV_SURV_PHASES 22 -> 25)
+#define MV_COMBINE_STEP(CTRL)                                                           \
+  {                                                                                     \
+    const double ov = dpp_f64<CTRL>(v);                                                 \
+    const int oi = dpp_i32<CTRL>(ix);                                                   \
+    const double ow = dpp_f64<CTRL>(w);                                                 \
+    if (ov < v || (ov == v && oi < ix)) {                                               \
+      v = ov;                                                                           \
+      ix = oi;                                                                          \
+    }                                                                                   \
+    w = max_prop(w, ow);                                                                \
+  }
+        MV_COMBINE_STEP(0xB1)
+        MV_COMBINE_STEP(0x4E)
+        MV_COMBINE_STEP(0x141)
+        MV_COMBINE_STEP(0x140)
+#undef MV_COMBINE_STEP
         cix[i] = ix;
         cw[i] = w;
       }
