@@ -434,16 +434,49 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     const int orow = rdl(orow_v, MV_IDX(k, min(nrw, 64), CK_GEN_LANE));
     if (a.genes_out) {
       double* gout = a.genes_out + (size_t)b * a.out_rows * V;
+      if constexpr (FUSED) {
+        // through a buffer resource over the child's row: the lanes past V fall outside its
+        // range and the hardware drops their stores (no per-register exec-mask branches)
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            gout + (size_t)orow * V, (short)0, Vo * 8, 0x00020000);
+        if (MV_CHECKS_ON) (void)MV_IDX((long long)orow, (long long)a.out_rows, CK_AT_CHILD);
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (lane + 64 * t < Vo)
-          gout[MV_IDX((size_t)orow * V + lane + 64 * t, (long long)a.out_rows * V, CK_AT_CHILD)] =
-              x[t];
+        for (int t = 0; t < NT; ++t) {
+          u32x2 w;
+          w.x = (unsigned)__double2loint(x[t]);
+          w.y = (unsigned)__double2hiint(x[t]);
+          __builtin_amdgcn_raw_buffer_store_b64(w, rr, 8u * (unsigned)lane + 512u * t, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (lane + 64 * t < Vo)
+            gout[MV_IDX((size_t)orow * V + lane + 64 * t, (long long)a.out_rows * V, CK_AT_CHILD)] =
+                x[t];
+      }
     }
     if (!ev) return;
     float* xo = a.xml + ((size_t)b * a.n + i) * Dm4;
     double acc = 0.0;
-    if (IDENT) {  // gene g <-> mutable feature g: no decoding
+    if (IDENT && FUSED && !REGC && p.xml_direct) {  // f2 only, branch-free -- every lane
+      // computes its term from in-range LDS reads and the sum takes +0.0 past Dm (acc >= +0,
+      // never -0: the bits are those of the guarded sum)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int j = lane + 64 * t;
+        const int jc = j < Dmo ? j : Dmo - 1;
+        const double xf = x[t];
+        const double d = (xf * s_es[jc] + s_em[jc]) - s_x0[jc];
+        if (l2) {
+          const double dd = d * d;
+          acc = acc + (j < Dmo ? dd : 0.0);
+        } else {
+          const double m = nanmax(acc, fabs(d));
+          acc = j < Dmo ? m : acc;
+        }
+      }
+    } else if (IDENT) {  // gene g <-> mutable feature g: no decoding
       const bool wx = !p.xml_direct;  // else k_mlp2 scales the child genes itself
       float* xd = xo;
 #pragma unroll
@@ -483,9 +516,9 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
       wave_sync();  // the next row's scatter overwrites xrow
     }
     if constexpr (FUSED) {  // the child into the wave's row buffer for the program below
+      // (padded to whole registers, o.rbs: the lanes past V write slots no op reads)
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (lane + 64 * t < Vo) frow[lane + 64 * t] = x[t];
+      for (int t = 0; t < NT; ++t) frow[lane + 64 * t] = x[t];
     }
     acc = l2 ? wave_sum(acc) : wave_max(acc);
     double f3 = 0.0;

@@ -44,7 +44,7 @@ struct VaryOff {
   unsigned xi, x_end;                             // region X at 0
   unsigned es, em, x0, e_at, sb;                  // region E at e_at; sb = blob bytes
   unsigned rb;                                    // ML row buffer bytes
-  unsigned rbs;                                   // slim row buffer bytes (Dm doubles)
+  unsigned rbs;                                   // slim row buffer bytes (Dm doubles, padded to 64)
 };
 __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   VaryOff o{};
@@ -98,7 +98,8 @@ __host__ __device__ inline VaryOff vary_offsets(const DProblem& p) {
   o.x0 = take(Dm4 * 8);
   o.sb = kb(off);
   o.rb = (unsigned)(((size_t)p.D * 8 + 15) & ~(size_t)15);
-  o.rbs = (unsigned)(((size_t)p.Dm * 8 + 15) & ~(size_t)15);
+  // whole 64-gene registers: k_genc writes every lane of its row registers unconditionally
+  o.rbs = (unsigned)(((size_t)p.Dm + 63) / 64 * 64 * 8);
   return o;
 }
 // k_gen keeps the ML-scaler / encoder coefficients of its genes in registers for IDENT
