@@ -462,18 +462,26 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (IDENT && FUSED && !REGC && p.xml_direct) {  // f2 only, branch-free -- every lane
       // computes its term from in-range LDS reads and the sum takes +0.0 past Dm (acc >= +0,
       // never -0: the bits are those of the guarded sum)
+      // (unclamped reads at immediate offsets: past Dm4 an index reads the next array of
+      // region E, and past x0 at most 64 NT - Dm4 doubles into the wave row buffers that
+      // follow it -- inside the allocation; those lanes' terms are never selected)
+      double dv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int j = lane + 64 * t;
-        const int jc = j < Dmo ? j : Dmo - 1;
-        const double xf = x[t];
-        const double d = (xf * s_es[jc] + s_em[jc]) - s_x0[jc];
-        if (l2) {
-          const double dd = d * d;
-          acc = acc + (j < Dmo ? dd : 0.0);
-        } else {
-          const double m = nanmax(acc, fabs(d));
-          acc = j < Dmo ? m : acc;
+        dv[t] = (x[t] * s_es[j] + s_em[j]) - s_x0[j];
+      }
+      if (l2) {  // the norm's branch outside the genes (one uniform branch per row)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const double dd = dv[t] * dv[t];
+          acc = acc + (lane + 64 * t < Dmo ? dd : 0.0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const double m = nanmax_sel(acc, fabs(dv[t]));
+          acc = lane + 64 * t < Dmo ? m : acc;
         }
       }
     } else if (IDENT) {  // gene g <-> mutable feature g: no decoding

@@ -811,8 +811,9 @@ __device__ __forceinline__ void apply_row_mutations(double* x, int nmut, int mpo
                                                     int k, int lane) {
 #pragma unroll
   for (int q = 0; q < CAP; ++q) {
+    if (q >= nmut) break;  // (uniform: no readlane for the absent slots)
     const int pr = rdl(mposv, CAP * k + q);  // stored gene; -1: a fixed gene (compact layout)
-    if (q < nmut && pr >= 0) {
+    if (pr >= 0) {
       const int pos = MV_IDX(pr, 64 * NT, CK_GEN_APPLY);
       const double y = rdl_d(mvalv, CAP * k + q);
       const int tt = pos >> 6;

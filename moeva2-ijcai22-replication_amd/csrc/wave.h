@@ -51,6 +51,13 @@ __device__ __forceinline__ double nanmax(double a, double b) {
   return b > a ? b : a;
 }
 
+// nanmax as selects (no exec-mask branches): the same value for every input
+__device__ __forceinline__ double nanmax_sel(double a, double b) {
+  double r = b > a ? b : a;
+  r = b != b ? b : r;
+  return a != a ? a : r;
+}
+
 template <class Op>
 __device__ __forceinline__ double wave_reduce(double v, Op op) {
   v = op(v, dpp_f64<0xB1>(v));
