@@ -124,15 +124,15 @@ __device__ __forceinline__ void wave_argbest(double& v, int& i, Better better) {
 }
 
 __device__ __forceinline__ double wave_max(double v) {
-  v = nanmax(v, dpp_f64<0xB1>(v));
-  v = nanmax(v, dpp_f64<0x4E>(v));
-  v = nanmax(v, dpp_f64<0x141>(v));
-  v = nanmax(v, dpp_f64<0x140>(v));
+  v = nanmax_sel(v, dpp_f64<0xB1>(v));
+  v = nanmax_sel(v, dpp_f64<0x4E>(v));
+  v = nanmax_sel(v, dpp_f64<0x141>(v));
+  v = nanmax_sel(v, dpp_f64<0x140>(v));
   double d0, d1;
   swap_f64<16>(v, d0, d1);
-  v = nanmax(d0, d1);
+  v = nanmax_sel(d0, d1);
   swap_f64<32>(v, d0, d1);
-  return nanmax(d0, d1);
+  return nanmax_sel(d0, d1);
 }
 
 // LDS byte addresses held in registers: lds_addr of a pointer into the kernel's LDS, and a
