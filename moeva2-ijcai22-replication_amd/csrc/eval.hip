@@ -434,7 +434,7 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     const int orow = rdl(orow_v, MV_IDX(k, min(nrw, 64), CK_GEN_LANE));
     if (a.genes_out) {
       double* gout = a.genes_out + (size_t)b * a.out_rows * V;
-      if constexpr (FUSED) {
+      if constexpr (IDENT) {
         // through a buffer resource over the child's row: the lanes past V fall outside its
         // range and the hardware drops their stores (no per-register exec-mask branches)
         typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -459,17 +459,19 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
     if (!ev) return;
     float* xo = a.xml + ((size_t)b * a.n + i) * Dm4;
     double acc = 0.0;
-    if (IDENT && FUSED && !REGC && p.xml_direct) {  // f2 only, branch-free -- every lane
+    if (IDENT && !REGC && p.xml_direct) {  // f2 only, branch-free -- every lane
       // computes its term from in-range LDS reads and the sum takes +0.0 past Dm (acc >= +0,
       // never -0: the bits are those of the guarded sum)
-      // (unclamped reads at immediate offsets: past Dm4 an index reads the next array of
-      // region E, and past x0 at most 64 NT - Dm4 doubles into the wave row buffers that
-      // follow it -- inside the allocation; those lanes' terms are never selected)
+      // (FUSED: unclamped reads at immediate offsets -- past Dm4 an index reads the next
+      // array of region E, and past x0 at most 64 NT - Dm4 doubles into the wave row buffers
+      // that follow it, inside the allocation; those lanes' terms are never selected.  The
+      // other layouts end at region E: their indices are clamped)
       double dv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int j = lane + 64 * t;
-        dv[t] = (x[t] * s_es[j] + s_em[j]) - s_x0[j];
+        const int jc = FUSED ? j : (j < Dmo ? j : Dmo - 1);
+        dv[t] = (x[t] * s_es[jc] + s_em[jc]) - s_x0[jc];
       }
       if (l2) {  // the norm's branch outside the genes (one uniform branch per row)
 #pragma unroll
