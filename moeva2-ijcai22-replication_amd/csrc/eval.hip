@@ -530,9 +530,9 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
 #pragma unroll
       for (int t = 0; t < NT; ++t) frow[lane + 64 * t] = x[t];
     }
-    acc = l2 ? wave_sum(acc) : wave_max(acc);
     double f3 = 0.0;
     double* hrow = nullptr;
+    bool reduced = false;
     if constexpr (FUSED) {  // k_cons's do_row on the registers' child (cons_rows, SLIM)
       wave_sync();
       hrow = a.hist ? a.hist + ((size_t)b * a.hist_rows +
@@ -540,8 +540,20 @@ __device__ __forceinline__ int gen_rows(const RowsArgs& a, int gen, int hist_row
                     : nullptr;
       double* hc = (hrow && a.hist_w > 3) ? hrow + 3 : nullptr;
       double* grow = a.G ? a.G + ((size_t)b * a.n + i) * p.C : nullptr;
-      f3 = constraints_slim(ftab, fso, fsrow, lane, grow, hc);
+      if (fso.sd_reg) {  // f2's sum, the lane ops' f3 part and the sum-diff columns in ONE
+                         // butterfly (wave_sum4: each total bit-identical to wave_sum's)
+        double a3, sdv[SD_REG], tot[4];
+        constraints_slim_parts(ftab, fso, lane, grow, hc, a3, sdv);
+        wave_sum4(l2 ? acc : 0.0, a3, sdv[0], sdv[1], lane, tot);
+        acc = l2 ? tot[0] : wave_max(acc);
+        const double sdt[SD_REG] = {tot[2], tot[3]};
+        f3 = constraints_slim_finish(ftab, lane, grow, hc, tot[1], sdt);
+        reduced = true;
+      } else {
+        f3 = constraints_slim(ftab, fso, fsrow, lane, grow, hc);
+      }
     }
+    if (!reduced) acc = l2 ? wave_sum(acc) : wave_max(acc);
     if (lane == 0) {
       double f2 = l2 ? sqrt(acc) : acc;
       if (p.scale_obj) f2 = f2 * p.f2_scale + 0.0;

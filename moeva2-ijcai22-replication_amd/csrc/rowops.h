@@ -349,6 +349,71 @@ __device__ __forceinline__ double constraints_slim(const OpTab& t, const SlimOps
   return wave_sum(acc3) + sdsum;
 }
 
+// constraints_slim in two halves around a batched reduction (k_genc, so.sd_reg): the lane
+// ops' partial f3 (acc3) and each ABS_SUMDIFF column's lane value ((0 + l) - r, 0 past the
+// program's columns) -- then, from their wave totals, the sum-diff columns' stores and f3,
+// in constraints_slim's order.
+__device__ __forceinline__ void constraints_slim_parts(const OpTab& t, const SlimOps& so, int lane,
+                                                       double* grow, double* hcols, double& acc3,
+                                                       double (&sdv)[SD_REG]) {
+  double va[OPS_REG], vb[OPS_REG];
+#pragma unroll
+  for (int k = 0; k < OPS_REG; ++k) {
+    va[k] = lds_ld(so.oa[k]);
+    vb[k] = lds_ld(so.ob[k]);
+  }
+  const double tol = t.tol;
+  acc3 = 0.0;
+  auto lane_ops = [&](auto st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < OPS_REG; ++k) {
+      const int c = lane + 64 * k;
+      double v = va[k] - vb[k];
+      if ((so.rg >> k) & 1)
+        if ((so.rbits >> k) & 1) v = (vb[k] != 0.0 ? va[k] / vb[k] : 0.0) - t.k1[c];
+      const double g = v <= tol ? 0.0 : v;
+      if (decltype(st)::value && c < t.n_lane) {
+        const int col = MV_IDX(t.col[c], t.C, CK_CONS_COL);
+        if (grow) grow[col] = g;
+        if (hcols) *MV_PTR(hcols + col, t.hlo, t.hhi, CK_AT_HIST2) = g;
+      }
+      acc3 += g;
+    }
+  };
+  if (grow || hcols)
+    lane_ops(std::true_type{});
+  else
+    lane_ops(std::false_type{});
+  const int nsd = t.C - t.n_lane;
+#pragma unroll
+  for (int j = 0; j < SD_REG; ++j) {
+    const double l = lds_ld(so.sdl[j]);
+    const double r = lds_ld(so.sdr[j]);
+    sdv[j] = j < nsd ? (0.0 + l) - r : 0.0;
+  }
+}
+__device__ __forceinline__ double constraints_slim_finish(const OpTab& t, int lane, double* grow,
+                                                          double* hcols, double acc3_total,
+                                                          const double (&sd_total)[SD_REG]) {
+  const double tol = t.tol;
+  double sdsum = 0.0;
+  const int nsd = t.C - t.n_lane;
+#pragma unroll
+  for (int j = 0; j < SD_REG; ++j) {
+    if (j < nsd) {
+      const int c = t.n_lane + j;
+      const double v = fabs(sd_total[j]);
+      const double g = v <= tol ? 0.0 : v;
+      if (lane == 0) {
+        if (grow) grow[t.col[c]] = g;
+        if (hcols) *MV_PTR(hcols + MV_IDX(t.col[c], t.C, CK_CONS_COL), t.hlo, t.hhi, CK_AT_HIST2) = g;
+      }
+      sdsum += g;
+    }
+  }
+  return acc3_total + sdsum;
+}
+
 // pymoo PolynomialMutation for one gene (softmax_mutation.py:77-103), no FMA contraction,
 // det_pow (detmath.h; its bit-identical FMA-product form) for np.power.
 __device__ __forceinline__ double poly_mut(double x, double xl, double xu, double u, double eta) {

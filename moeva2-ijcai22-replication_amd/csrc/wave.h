@@ -51,6 +51,40 @@ __device__ __forceinline__ double nanmax(double a, double b) {
   return b > a ? b : a;
 }
 
+// Four wave sums in one butterfly (k_genc's row: f2, the lane ops' f3 part and two
+// ABS_SUMDIFF columns).  Each total is the same pairwise tree as wave_sum's -- blocks of 1, 2,
+// 4, 8, 16, 32 lanes -- so its bits are wave_sum's (a + b == b + a; only which lane holds a
+// block sum differs): level 1 keeps values 0, 1 on even lanes and 2, 3 on odd ones, level 2
+// one value per lane (lane bits (0, 1) -> value 0, 1, 2, 3 on lanes 0, 2, 1, 3), levels 3 and
+// 4 shift the higher block down the row (row_shl 4, 8: lanes 0-3 collect), levels 5 and 6
+// are wave_sum's row swaps.  About 35 VALU instead of four wave_sums' 72.
+__device__ __forceinline__ double rdl_f64(double v, int k) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), k);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), k);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void wave_sum4(double v0, double v1, double v2, double v3, int lane,
+                                          double (&t)[4]) {
+  const bool odd = (lane & 1) != 0, b1 = (lane & 2) != 0;
+  const double k0 = odd ? v2 : v0, k1 = odd ? v3 : v1;  // kept
+  const double s0 = odd ? v0 : v2, s1 = odd ? v1 : v3;  // the partner's values
+  const double a0 = k0 + dpp_f64<0xB1>(s0);
+  const double a1 = k1 + dpp_f64<0xB1>(s1);
+  const double kk = b1 ? a1 : a0, ss = b1 ? a0 : a1;
+  double w = kk + dpp_f64<0x4E>(ss);
+  w = w + dpp_f64<0x104>(w);  // row_shl:4 -- lane i + 4's block
+  w = w + dpp_f64<0x108>(w);  // row_shl:8
+  double d0, d1;
+  swap_f64<16>(w, d0, d1);
+  w = d0 + d1;
+  swap_f64<32>(w, d0, d1);
+  w = d0 + d1;
+  t[0] = rdl_f64(w, 0);
+  t[1] = rdl_f64(w, 2);
+  t[2] = rdl_f64(w, 1);
+  t[3] = rdl_f64(w, 3);
+}
+
 // nanmax as selects (no exec-mask branches): the same value for every input
 __device__ __forceinline__ double nanmax_sel(double a, double b) {
   double r = b > a ? b : a;
