@@ -694,7 +694,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     for (;;) {
       int t = 0;
       if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
-      t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+      t = __builtin_amdgcn_readfirstlane(t);  // lane 0 is the first active lane
       if (t >= n_b) break;
       int qi = 0, rem = t;
       while (rem >= NW - qi) {
@@ -719,7 +719,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
     for (;;) {
       int t = 0;
       if (lane == 0) t = atomicAdd(&L.iscal[14], 1);
-      t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
+      t = __builtin_amdgcn_readfirstlane(t);  // lane 0 is the first active lane
       if (t >= n_q) break;
       const int qq = t & 3;
       int qi = 0, rem = t >> 2;
@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
         if (odd) b0 = __builtin_fmin(b0, d2f(RN - 1));
       }
       double best = __builtin_fmin(__builtin_fmin(b0, b1), __builtin_fmin(b2, b3));
-      best = __builtin_fmin(best, __shfl_xor(best, 1, 64));
+      best = __builtin_fmin(best, dpp_f64<0xB1>(best));  // the pair's other lane (DPP xor 1)
       const double lim = best + 1e-14 * (nn + best);
       if (lim < __builtin_inf()) {  // false on NaN / inf (the same in both lanes)
         double bd = __builtin_inf();
@@ -1134,15 +1134,15 @@ __device__ __forceinline__ void survive_state(const SurvArgs& a, const int b, co
             if (odd && d2f(RN - 1) <= lim) hit(RN - 1);
           }
         }
-        const bool ovf = nc > 4 || __shfl_xor(nc, 1, 64) > 4;
+        const bool ovf = nc > 4 || dpp_i32<0xB1>(nc) > 4;
         if (!ovf) {
           if (nc > 0) cand(c0);
           if (nc > 1) cand(c1);
           if (nc > 2) cand(c2);
           if (nc > 3) cand(c3);
         }
-        const double od = __shfl_xor(bd, 1, 64);
-        const int oj = __shfl_xor(bj, 1, 64);
+        const double od = dpp_f64<0xB1>(bd);
+        const int oj = dpp_i32<0xB1>(bj);
         if (arg_better(od, oj, bd, bj)) {
           bd = od;
           bj = oj;
