@@ -1115,7 +1115,10 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 0;
     (void)hipGetLastError();
-    sa.wide = B <= 2 * cus ? 1 : 0;
+    // 2: small attacks (every state has half a CU or more to itself -- configs[0], the
+    // per-GPU share of 8-GPU strong scaling): 16-wave workgroups, so one state's issue-
+    // and latency-bound phases interleave four waves per SIMD
+    sa.wide = 2 * B <= cus ? 2 : B <= 2 * cus ? 1 : 0;
     if (const char* w = std::getenv("MV_SURV_WIDE")) sa.wide = std::atoi(w);  // A/B
   }
   if (use_plan) {

@@ -196,7 +196,8 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   const int n_m = a.parents_out ? (a.O_next + 1) / 2 : 0;
   const int pslots = a.parents_out ? ((n_m * 4 + a.n_survive - 1) / a.n_survive) * a.n_survive : 1;
   static const size_t pad = lds_pad("MV_LDS_PAD_SURV");
-  const int T = a.N > SURV_NLDS ? SURV_T_BIG : (a.wide ? SURV_T_MID : SURV_T);
+  const int T = a.N > SURV_NLDS ? SURV_T_BIG
+                                : (a.wide == 2 ? SURV_T_BIG : a.wide ? SURV_T_MID : SURV_T);
   const size_t lds =
       surv_lds_bytes(a.N, a.R, pslots, a.plan_hdr ? plan_tab_words(a.Vr, a.V) : 0, T) + pad;
   static bool configured = false;
@@ -207,11 +208,16 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k_survive<SURV_NMAX / 64, SURV_T_BIG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_survive<SURV_NLDS / 64, SURV_T_BIG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     configured = true;
   }
   if (a.N <= SURV_NLDS) {
-    if (T == SURV_T_MID)
+    if (T == SURV_T_BIG)
+      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
+                         stream, a);
+    else if (T == SURV_T_MID)
       hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T_MID>), dim3(B), dim3(SURV_T_MID), lds,
                          stream, a);
     else
