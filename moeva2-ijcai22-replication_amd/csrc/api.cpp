@@ -20,6 +20,10 @@
 
 using namespace mv;
 
+namespace mv {
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;  // kernels.h MV_LAUNCH
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -200,6 +204,10 @@ struct mv_engine {
   int attack_mode = 0;      // 0: auto, 1: per-phase chain (the only schedule)
   bool profiling = false;
   std::vector<hipEvent_t> ev_var, ev_cons, ev_mlp, ev_surv;
+  // kernel-exact profiling pairs per recorded generation: k_gen(c) start / stop, k_cons start /
+  // stop, classifier start / stop (hipExtLaunchKernelGGL stamps, kernels.h MV_LAUNCH); the
+  // survival pair is ev_surv
+  std::vector<hipEvent_t> ev_kx;
   int n_var_rec = 0, n_surv_rec = 0;
 
   void free_list(std::vector<void*>& v) {
@@ -229,6 +237,7 @@ struct mv_engine {
     }
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     for (auto e : ev_surv) (void)hipEventDestroy(e);
+    for (auto e : ev_kx) (void)hipEventDestroy(e);
     (void)hipGetLastError();  // do not leave a teardown status for the next launch check
   }
 };
@@ -1161,6 +1170,7 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     if (ensure_events(e->ev_mlp, (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_cons, (size_t)G) != MV_OK) return MV_ERR_HIP;
     if (ensure_events(e->ev_surv, 2 * (size_t)G) != MV_OK) return MV_ERR_HIP;
+    if (ensure_events(e->ev_kx, 6 * (size_t)G) != MV_OK) return MV_ERR_HIP;
   }
   e->n_var_rec = 0;
   e->n_surv_rec = 0;
@@ -1211,16 +1221,41 @@ int mv_attack_run(mv_engine* e, const mv_attack_params* prm, void* stream_) {
     for (int q = 0; q < ngrp; ++q) {
       hipStream_t st = gs[q];
       const bool prof = e->profiling && q == 0;
-      if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec], st));
+      // profiled steps: each launch takes an armed event pair (kernel-exact stamps); a step
+      // that launches no kernel (k_genc's empty k_cons) records the pair back to back
+      struct Disarm {
+        ~Disarm() { g_ev_start = g_ev_stop = nullptr; }
+      } disarm;
+      auto arm = [&](hipEvent_t a0, hipEvent_t a1) {
+        g_ev_start = a0;
+        g_ev_stop = a1;
+      };
+      auto settle = [&]() -> hipError_t {
+        if (!g_ev_start) return hipSuccess;
+        hipError_t r = hipEventRecord(g_ev_start, st);
+        if (r == hipSuccess) r = hipEventRecord(g_ev_stop, st);
+        g_ev_start = g_ev_stop = nullptr;
+        return r;
+      };
+      hipEvent_t* kx = prof ? &e->ev_kx[6 * (size_t)e->n_var_rec] : nullptr;
+      if (prof) arm(kx[0], kx[1]);
       HIPCHK(launch_gen(vq[q], slot_va[q], g, hist_row0, st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_cons[e->n_var_rec], st));
+      if (prof) HIPCHK(settle());
+      if (prof) arm(kx[2], kx[3]);
       HIPCHK(launch_cons(vq[q], slot_va[q], hist_row0, st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_var[2 * e->n_var_rec + 1], st));
+      if (prof) HIPCHK(settle());
+      if (prof) arm(kx[4], kx[5]);
       HIPCHK(launch_mlp(vq[q], slot_va[q], hist_row0, st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_mlp[e->n_var_rec++], st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec], st));
+      if (prof) {
+        HIPCHK(settle());
+        ++e->n_var_rec;
+        arm(e->ev_surv[2 * (size_t)e->n_surv_rec], e->ev_surv[2 * (size_t)e->n_surv_rec + 1]);
+      }
       HIPCHK(launch_survive(group_surv(sa, q), gb0[q + 1] - gb0[q], st));
-      if (prof) HIPCHK(hipEventRecord(e->ev_surv[2 * e->n_surv_rec++ + 1], st));
+      if (prof) {
+        HIPCHK(settle());
+        ++e->n_surv_rec;
+      }
     }
   }
   for (int q = 0; q < ngrp; ++q) HIPCHK(release_rows(slot_va[q], gs[q]));
@@ -1251,12 +1286,14 @@ int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* s
                         int32_t* n_generations) {
   if (!e) return fail(MV_ERR_ARG, "null engine");
   double tv = 0.0, tm = 0.0, ts = 0.0;
-  for (int i = 0; i < e->n_var_rec; ++i) {
-    float ms = 0.f, ms2 = 0.f;
-    HIPCHK(hipEventSynchronize(e->ev_mlp[i]));
-    HIPCHK(hipEventElapsedTime(&ms, e->ev_var[2 * i], e->ev_var[2 * i + 1]));
-    HIPCHK(hipEventElapsedTime(&ms2, e->ev_var[2 * i + 1], e->ev_mlp[i]));
-    tv += ms;
+  for (int i = 0; i < e->n_var_rec; ++i) {  // kernel-exact pairs (ev_kx)
+    float ms = 0.f, ms1 = 0.f, ms2 = 0.f;
+    const hipEvent_t* kx = &e->ev_kx[6 * (size_t)i];
+    HIPCHK(hipEventSynchronize(kx[5]));
+    HIPCHK(hipEventElapsedTime(&ms, kx[0], kx[1]));
+    HIPCHK(hipEventElapsedTime(&ms1, kx[2], kx[3]));
+    HIPCHK(hipEventElapsedTime(&ms2, kx[4], kx[5]));
+    tv += (double)ms + ms1;
     tm += ms2;
   }
   for (int i = 0; i < e->n_surv_rec; ++i) {
@@ -1408,10 +1445,11 @@ int mv_get_phase_times(mv_engine* e, double* ms, int32_t* n_generations) {
   double t[4] = {0, 0, 0, 0};
   for (int i = 0; i < e->n_var_rec; ++i) {
     float a = 0.f, b = 0.f, c = 0.f;
-    HIPCHK(hipEventSynchronize(e->ev_mlp[i]));
-    HIPCHK(hipEventElapsedTime(&a, e->ev_var[2 * i], e->ev_cons[i]));
-    HIPCHK(hipEventElapsedTime(&b, e->ev_cons[i], e->ev_var[2 * i + 1]));
-    HIPCHK(hipEventElapsedTime(&c, e->ev_var[2 * i + 1], e->ev_mlp[i]));
+    const hipEvent_t* kx = &e->ev_kx[6 * (size_t)i];
+    HIPCHK(hipEventSynchronize(kx[5]));
+    HIPCHK(hipEventElapsedTime(&a, kx[0], kx[1]));
+    HIPCHK(hipEventElapsedTime(&b, kx[2], kx[3]));
+    HIPCHK(hipEventElapsedTime(&c, kx[4], kx[5]));
     t[0] += a;
     t[1] += b;
     t[2] += c;

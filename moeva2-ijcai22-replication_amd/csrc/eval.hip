@@ -2451,7 +2451,7 @@ hipError_t launch_decode(const DProblem& p, const DStates& s, int B, int n, cons
   if (total <= 0) return hipSuccess;
   long blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(256), 0, stream, p.fdec, s.x_init, B,
+  MV_LAUNCH(k_decode, dim3((unsigned)blocks), dim3(256), 0, stream, p.fdec, s.x_init, B,
                      n, p.V, p.D, genes, x);
   return hipGetLastError();
 }
@@ -2633,9 +2633,9 @@ static hipError_t gen_go(dim3 grid, size_t lds, hipStream_t s, int slot, int gen
     configured = true;
   }
   if (sbx)
-    hipLaunchKernelGGL((k_gen<IDENT, NT, true>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+    MV_LAUNCH((k_gen<IDENT, NT, true>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
   else
-    hipLaunchKernelGGL((k_gen<IDENT, NT, false>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
+    MV_LAUNCH((k_gen<IDENT, NT, false>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw);
   return hipGetLastError();
 }
 
@@ -2646,7 +2646,7 @@ static hipError_t cons_go(dim3 grid, size_t lds, hipStream_t s, int slot, int h0
     allow_lds(k_cons<FULL, IDENT, NT>);
     configured = true;
   }
-  hipLaunchKernelGGL((k_cons<FULL, IDENT, NT>), grid, dim3(CONS_T), lds, s, slot, h0, rw);
+  MV_LAUNCH((k_cons<FULL, IDENT, NT>), grid, dim3(CONS_T), lds, s, slot, h0, rw);
   return hipGetLastError();
 }
 
@@ -2669,7 +2669,7 @@ static hipError_t narrow_go(const RowsArgs& a, int slot, int gen, int hist_row0,
   }
   const size_t lds = narrow_lds(vary_offsets(a.p), a.p).total;
   const dim3 grid((unsigned)((a.total + NARROW_T - 1) / NARROW_T));
-  hipLaunchKernelGGL((k_narrow<NV, FULL>), grid, dim3(NARROW_T), lds, stream, slot, gen,
+  MV_LAUNCH((k_narrow<NV, FULL>), grid, dim3(NARROW_T), lds, stream, slot, gen,
                      hist_row0);
   return hipGetLastError();
 }
@@ -2713,7 +2713,7 @@ static hipError_t genc_go(dim3 grid, size_t lds, hipStream_t s, int slot, int ge
     configured = true;
   }
 #define GENC(X, Y) \
-  hipLaunchKernelGGL((k_genc<true, NT, X, Y>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw)
+  MV_LAUNCH((k_genc<true, NT, X, Y>), grid, dim3(VARY_T), lds, s, slot, gen, h0, rw)
   if (sbx) {
     if (slim)
       GENC(true, true);
@@ -2858,7 +2858,7 @@ static hipError_t mlp2_go3(const RowsArgs& a, int slot, int hist_row0, hipStream
   }
   const int ntiles = (a.total + M2_ROWS - 1) / M2_ROWS;
   const int grid = ntiles < occ * cu_count() ? ntiles : occ * cu_count();
-  hipLaunchKernelGGL((k_mlp2<CJ, BF, DIRECT, CO>), dim3(grid), dim3(256), lds, stream, slot,
+  MV_LAUNCH((k_mlp2<CJ, BF, DIRECT, CO>), dim3(grid), dim3(256), lds, stream, slot,
                      hist_row0);
   return hipGetLastError();
 }
@@ -2891,7 +2891,7 @@ static hipError_t mlpr_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   const int ntiles = (a.total + 16 * RW - 1) / (16 * RW);
   const int need = (ntiles + 3) / 4;
   const int grid = need < occ * cu_count() ? need : occ * cu_count();
-  hipLaunchKernelGGL((k_mlpr<RW, NO>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
+  MV_LAUNCH((k_mlpr<RW, NO>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
@@ -2915,7 +2915,7 @@ static hipError_t mlpw_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   const size_t lds = mlpw_lds(a.p).total;
   const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
   const int grid = ntiles < cu_count() ? ntiles : cu_count();  // one 133-KiB workgroup per CU
-  hipLaunchKernelGGL((k_mlpw<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
+  MV_LAUNCH((k_mlpw<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
@@ -2929,7 +2929,7 @@ static hipError_t mlpw32_go(const RowsArgs& a, int slot, int hist_row0, hipStrea
   const size_t lds = mlpw32_lds(a.p).total;
   const int ntiles = (a.total + MW_ROWS - 1) / MW_ROWS;
   const int grid = ntiles < cu_count() ? ntiles : cu_count();  // one workgroup per CU
-  hipLaunchKernelGGL((k_mlpw32<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
+  MV_LAUNCH((k_mlpw32<CJ>), dim3(grid), dim3(MW_T), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
@@ -2991,9 +2991,9 @@ hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t st
 #define MLP(M)                                                                           \
   {                                                                                      \
     if (a.p.mlp_bf16)                                                                    \
-      hipLaunchKernelGGL((k_mlp<M, true>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
+      MV_LAUNCH((k_mlp<M, true>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
     else                                                                                 \
-      hipLaunchKernelGGL((k_mlp<M, false>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
+      MV_LAUNCH((k_mlp<M, false>), grid, dim3(EVAL_T), lds, stream, slot, hist_row0); \
   }
   if (nct <= 4)
     MLP(1)
@@ -3026,13 +3026,13 @@ static hipError_t predict_go(const MlpArgs& a, int nct, size_t lds, hipStream_t 
   }
   const dim3 grid((a.n + 16 * RT - 1) / (16 * RT));
   if (nct <= 4)
-    hipLaunchKernelGGL((k_predict<1, RT>), grid, dim3(EVAL_T), lds, stream, a);
+    MV_LAUNCH((k_predict<1, RT>), grid, dim3(EVAL_T), lds, stream, a);
   else if (nct <= 8)
-    hipLaunchKernelGGL((k_predict<2, RT>), grid, dim3(EVAL_T), lds, stream, a);
+    MV_LAUNCH((k_predict<2, RT>), grid, dim3(EVAL_T), lds, stream, a);
   else if (nct <= 16)
-    hipLaunchKernelGGL((k_predict<4, RT>), grid, dim3(EVAL_T), lds, stream, a);
+    MV_LAUNCH((k_predict<4, RT>), grid, dim3(EVAL_T), lds, stream, a);
   else
-    hipLaunchKernelGGL((k_predict<8, RT>), grid, dim3(EVAL_T), lds, stream, a);
+    MV_LAUNCH((k_predict<8, RT>), grid, dim3(EVAL_T), lds, stream, a);
   return hipGetLastError();
 }
 
@@ -3056,9 +3056,9 @@ hipError_t launch_constraints(const DProblem& hp, int slot, int n, const double*
   const size_t lds = (size_t)4 * hp.D * sizeof(double);
   const dim3 grid((n + 3) / 4);
   if (hp.full_ops)
-    hipLaunchKernelGGL(k_constraints<true>, grid, dim3(256), lds, stream, slot, n, x, G);
+    MV_LAUNCH(k_constraints<true>, grid, dim3(256), lds, stream, slot, n, x, G);
   else
-    hipLaunchKernelGGL(k_constraints<false>, grid, dim3(256), lds, stream, slot, n, x, G);
+    MV_LAUNCH(k_constraints<false>, grid, dim3(256), lds, stream, slot, n, x, G);
   return hipGetLastError();
 }
 
@@ -3069,7 +3069,7 @@ hipError_t launch_setup_states(int slot, int B, const double* x_init, const doub
                                double* gu, unsigned char* sblob, float* bias1, double* genes0,
                                hipStream_t stream) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_setup_states, dim3(B), dim3(256), 0, stream, slot, x_init, xl, xu, W1full,
+  MV_LAUNCH(k_setup_states, dim3(B), dim3(256), 0, stream, slot, x_init, xl, xu, W1full,
                      b1, gl, gu, sblob, bias1, genes0);
   return hipGetLastError();
 }

@@ -1,10 +1,29 @@
 // Launch wrappers shared by the C-ABI layer (api.cpp) and the kernel files.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "engine.h"
 
 namespace mv {
+
+// Kernel-exact profiling (mv_set_profiling): api.cpp sets a start / stop event pair before a
+// profiled launch; the next MV_LAUNCH hands them to hipExtLaunchKernelGGL, which stamps the
+// kernel's own start and end (events recorded around the launch would include the dispatch
+// gap: ~8 us per k_genc launch, so the bench's per-kernel times now agree with rocprofv3's),
+// and clears them.  Unset, MV_LAUNCH is hipLaunchKernelGGL.
+extern thread_local hipEvent_t g_ev_start, g_ev_stop;
+#define MV_LAUNCH(K, GRID, BLOCK, LDS, STREAM, ...)                                          \
+  do {                                                                                       \
+    if (::mv::g_ev_start) {                                                                  \
+      hipExtLaunchKernelGGL(K, GRID, BLOCK, LDS, STREAM, ::mv::g_ev_start, ::mv::g_ev_stop,  \
+                            0, __VA_ARGS__);                                                 \
+      ::mv::g_ev_start = nullptr;                                                            \
+      ::mv::g_ev_stop = nullptr;                                                             \
+    } else {                                                                                 \
+      hipLaunchKernelGGL(K, GRID, BLOCK, LDS, STREAM, __VA_ARGS__);                          \
+    }                                                                                        \
+  } while (0)
 
 // LDS of k_mlp / k_predict: head (32 row states + final-layer weights and bias) + R1 (A tile
 // / ping) + R2 (pong).

@@ -215,17 +215,17 @@ hipError_t launch_survive(const SurvArgs& a, int B, hipStream_t stream) {
   }
   if (a.N <= SURV_NLDS) {
     if (T == SURV_T_BIG)
-      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
+      MV_LAUNCH((k_survive<SURV_NLDS / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
                          stream, a);
     else if (T == SURV_T_MID)
-      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T_MID>), dim3(B), dim3(SURV_T_MID), lds,
+      MV_LAUNCH((k_survive<SURV_NLDS / 64, SURV_T_MID>), dim3(B), dim3(SURV_T_MID), lds,
                          stream, a);
     else
-      hipLaunchKernelGGL((k_survive<SURV_NLDS / 64, SURV_T>), dim3(B), dim3(SURV_T), lds, stream,
+      MV_LAUNCH((k_survive<SURV_NLDS / 64, SURV_T>), dim3(B), dim3(SURV_T), lds, stream,
                          a);
   } else {
     if (!a.dom_g || a.dom_stride < (size_t)a.N * ((a.N + 63) / 64)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_survive<SURV_NMAX / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
+    MV_LAUNCH((k_survive<SURV_NMAX / 64, SURV_T_BIG>), dim3(B), dim3(SURV_T_BIG), lds,
                        stream, a);
   }
   return hipGetLastError();
@@ -237,14 +237,14 @@ hipError_t launch_select(int B, int P, int O, uint64_t seed, uint32_t sk, int ge
   const int n_m = (O + 1) / 2;
   const int slots = ((n_m * 4 + P - 1) / P) * P;
   const size_t lds = (size_t)pow2_at_least(slots) * 8 + (size_t)slots * 4;
-  hipLaunchKernelGGL(k_select, dim3(B), dim3(SURV_T), lds, stream, P, O, seed, sk,
+  MV_LAUNCH(k_select, dim3(B), dim3(SURV_T), lds, stream, P, O, seed, sk,
                      gen, pop_slot, parents);
   return hipGetLastError();
 }
 
 hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* genes0, double* pool,
                             int* pop_slot, int* free_slot, hipStream_t stream) {
-  hipLaunchKernelGGL(k_init_pool, dim3(1024), dim3(256), 0, stream, B, P, O, V, S, genes0, pool,
+  MV_LAUNCH(k_init_pool, dim3(1024), dim3(256), 0, stream, B, P, O, V, S, genes0, pool,
                      pop_slot, free_slot);
   return hipGetLastError();
 }
@@ -252,7 +252,7 @@ hipError_t launch_init_pool(int B, int P, int O, int V, int S, const double* gen
 hipError_t launch_gather_pop(int B, int P, int V, int Vr, int S, const int* cmap,
                              const double* glr, const int* pop_slot, const double* pool,
                              const double* poolF, double* genes, double* F, hipStream_t stream) {
-  hipLaunchKernelGGL(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, Vr, S, cmap, glr,
+  MV_LAUNCH(k_gather_pop, dim3(2048), dim3(256), 0, stream, B, P, V, Vr, S, cmap, glr,
                      pop_slot, pool, poolF, genes, F);
   return hipGetLastError();
 }
@@ -263,11 +263,11 @@ hipError_t launch_front(int B, int P, int V, int Vr, int S, const int* cmap, con
                         hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   if (P < 1 || P > 1024 || !front || !offsets) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_front_mask, dim3(B), dim3(256), (size_t)P * 3 * sizeof(double), stream, P,
+  MV_LAUNCH(k_front_mask, dim3(B), dim3(256), (size_t)P * 3 * sizeof(double), stream, P,
                      S, pop_slot, poolF, front, offsets);
-  hipLaunchKernelGGL(k_front_scan, dim3(1), dim3(1024), 0, stream, B, offsets);
+  MV_LAUNCH(k_front_scan, dim3(1), dim3(1024), 0, stream, B, offsets);
   if (X || Fx)
-    hipLaunchKernelGGL(k_front_gather, dim3(B), dim3(256), 0, stream, P, V, Vr, S, cmap, glr,
+    MV_LAUNCH(k_front_gather, dim3(B), dim3(256), 0, stream, P, V, Vr, S, cmap, glr,
                        pop_slot, pool, poolF, front, offsets, X, Fx);
   return hipGetLastError();
 }

@@ -16,7 +16,7 @@ for n in $LIBS; do SETS="$SETS MOEVA_MI355X_LIB=$(path $n)"; done
 for w in $WORKLOADS; do
   for n in $LIBS; do
     MOEVA_MI355X_LIB=$(path $n) timeout -k 10 300 python -u bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-configs --no-generate > $O/$w.$n.json 2> $O/$w.$n.log || exit 1
-    echo "$w [$n]: $(python3 -c "import json;d=json.load(open('$O/$w.$n.json'));print(round(d['value']/1e6,2), 'M evals/s', {k: round(v*1000,1) for k,v in d['kernels_avg_ms_per_generation'].items() if k!='dominant'})")"
+    echo "$w [$n]: $(python3 -c "import json;d=json.load(open('$O/$w.$n.json'));print(round(d['value']/1e6,2), 'M evals/s', {k: round(v*1000,1) for k,v in d['kernels_avg_ms_per_generation'].items() if not isinstance(v, str)})")"
   done
 done
 for n in $PHASE_LIBS; do  # clocks builds (MV_CLOCKS=1), e.g. PHASE_LIBS="clk"
