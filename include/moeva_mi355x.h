@@ -272,9 +272,11 @@ int mv_gene_layout(mv_engine* e, int32_t B, const double* x_init, const double* 
  * batch.  mv_set_states fails with MV_ERR_ARG when an unstored gene is not fixed in a bound
  * state.  stored = NULL returns to deriving the layout from each bound batch (default). */
 int mv_set_gene_layout(mv_engine* e, const int32_t* stored, int32_t V);
-/* Per-kernel timing of the last mv_attack_run when enabled (one state group then): HIP
- * events recorded on the run's stream around the row kernel(s), the classifier and
- * k_survive of every generation (summed ms). */
+/* Per-kernel timing of the last mv_attack_run when enabled (one state group then): each
+ * profiled launch -- the row kernel(s), the classifier and k_survive of every generation --
+ * is made with hipExtLaunchKernelGGL and a start / stop HIP event pair, which stamp the
+ * kernel's own execution (no dispatch gap); summed ms.  A step that launches no kernel
+ * (k_cons under k_genc / k_narrow) reads 0. */
 int mv_set_profiling(mv_engine* e, int32_t enabled);
 int mv_get_kernel_times(mv_engine* e, double* vary_ms, double* mlp_ms, double* survive_ms,
                         int32_t* n_generations);
