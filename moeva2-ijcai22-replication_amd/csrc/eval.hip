@@ -1628,7 +1628,9 @@ __host__ __device__ inline MlprLds mlpr_lds(const DProblem& p, int rw) {
 // gene pairs), fp32, every MFMA layer's width a multiple of 16 and at most 64, K0 a multiple
 // of 16, at most 8 classes.
 __host__ __device__ inline bool mlpr_ok(const DProblem& p) {
-  if (!p.xml_direct || p.mlp_bf16 || !p.mlp2 || p.n_layers < 2 || (p.Dm & 1) || p.Dm < 2)
+  // the fp32 ML-row path (LCLD: k_narrow's xml rows, zero-padded to Dm4) takes the XML
+  // instance: the same tiles with the rows' fp32 values as layer 0's operands
+  if (p.mlp_bf16 || !p.mlp2 || p.n_layers < 2 || (p.xml_direct && ((p.Dm & 1) || p.Dm < 2)))
     return false;
   for (int l = 0; l + 1 < p.n_layers; ++l)
     if (!p.Wp[l]) return false;
@@ -1637,7 +1639,7 @@ __host__ __device__ inline bool mlpr_ok(const DProblem& p) {
   return p.Dm4 % 16 == 0 && p.dims[p.n_layers] <= 8 && mlpr_lds(p, 2).total <= 96 * 1024;
 }
 
-template <int RW, int NO>
+template <int RW, int NO, bool XML = false>
 __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slot, int hist_row0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowsArgs& a = c_rows[slot];
@@ -1655,10 +1657,11 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
   float* wl = (float*)(smem + L.wl);
   float* bl = wl + Klast * nout;
   float* hs = (float*)(smem + L.hs + wave * L.wst);
-  for (int q = tid; q < K0; q += 256) {
-    sS[q] = p.mlS[q];
-    sM[q] = p.mlM[q];
-  }
+  if (!XML)
+    for (int q = tid; q < K0; q += 256) {
+      sS[q] = p.mlS[q];
+      sM[q] = p.mlM[q];
+    }
   for (int q = tid; q < Klast * nout; q += 256) wl[q] = p.W[nl - 1][q];
   if (tid < nout) bl[tid] = p.bias[nl - 1][tid];
   float* hw = (float*)(smem + L.hw);
@@ -1683,6 +1686,7 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
       phq[6] = wall_clock64();
     }
     const double* grow[RW];
+    const float* xrw[RW];  // XML: the rows' fp32 ML values (xml [total][K0])
     int rst[RW];
 #pragma unroll
     for (int rt = 0; rt < RW; ++rt) {
@@ -1690,7 +1694,8 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
       const int rr = rr0 < a.total ? rr0 : a.total - 1;
       const int st = rr / a.n, i = rr - st * a.n;
       rst[rt] = st;
-      grow[rt] = a.mode == 1
+      xrw[rt] = a.xml + (size_t)rr * K0;
+      if (!XML) grow[rt] = a.mode == 1
           ? a.genes_out + ((size_t)st * a.out_rows +
                            MV_IDX(a.out_map ? a.out_map[rr] : i, a.out_rows, CK_MLP_ROW)) * Dm
           : a.genes_in + ((size_t)st * a.in_rows + MV_IDX(i, a.in_rows, CK_MLP_ROW)) * Dm;
@@ -1719,6 +1724,7 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
     // would wait for those genes too.
     float4 wA[4], wB[4];
     double2 g0[RW][2], g1[RW][2], g2[RW][2], g3[RW][2];
+    float4 f0[RW], f1[RW], f2[RW], f3[RW];  // XML
 #define MR_LOADW(kg, w)                                                                    \
   {                                                                                        \
     const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
@@ -1727,32 +1733,43 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
       w[nb] = *(const float4*)(Wp0 + ((size_t)kgc * N0 + nbc * 16 + il) * 16 + 4 * ka);    \
     }                                                                                      \
   }
-#define MR_LOADG(kg, g)                                                                    \
+#define MR_LOADG(kg, g, f)                                                                 \
   {                                                                                        \
     const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
     const int k = 16 * kgc + 4 * ka;                                                       \
-    const int k01 = k + 1 < Dm ? k : Dm - 2, k23 = k + 3 < Dm ? k + 2 : Dm - 2;            \
-    _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                    \
-      g[rt][0] = *(const double2*)(grow[rt] + k01);                                        \
-      g[rt][1] = *(const double2*)(grow[rt] + k23);                                        \
+    if constexpr (XML) {                                                                   \
+      _Pragma("unroll") for (int rt = 0; rt < RW; ++rt)                                    \
+        f[rt] = *(const float4*)(xrw[rt] + k);                                             \
+    } else {                                                                               \
+      const int k01 = k + 1 < Dm ? k : Dm - 2, k23 = k + 3 < Dm ? k + 2 : Dm - 2;          \
+      _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                  \
+        g[rt][0] = *(const double2*)(grow[rt] + k01);                                      \
+        g[rt][1] = *(const double2*)(grow[rt] + k23);                                      \
+      }                                                                                    \
     }                                                                                      \
   }
-#define MR_STEP(kg, w, g)                                                                  \
+#define MR_STEP(kg, w, g, f)                                                               \
   {                                                                                        \
     const int kgc = (kg) < nkg0 ? (kg) : nkg0 - 1;                                         \
     const int k = 16 * kgc + 4 * ka;                                                       \
-    const double2 s01 = *(const double2*)(sS + k), s23 = *(const double2*)(sS + k + 2);    \
-    const double2 m01 = *(const double2*)(sM + k), m23 = *(const double2*)(sM + k + 2);    \
-    const double sc[4] = {s01.x, s01.y, s23.x, s23.y}, mn[4] = {m01.x, m01.y, m23.x, m23.y}; \
     /* k >= Dm (the zero padding to K0) and the k-groups past nkg0: +0 */                  \
     unsigned msk[4];                                                                       \
     _Pragma("unroll") for (int e = 0; e < 4; ++e)                                          \
       msk[e] = (k + e < Dm && (kg) < nkg0) ? 0xFFFFFFFFu : 0u;                             \
     float xb[RW][4];                                                                       \
-    _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                    \
-      const double gv[4] = {g[rt][0].x, g[rt][0].y, g[rt][1].x, g[rt][1].y};               \
-      _Pragma("unroll") for (int e = 0; e < 4; ++e)                                        \
-        xb[rt][e] = __uint_as_float(__float_as_uint((float)(gv[e] * sc[e] + mn[e])) & msk[e]); \
+    if constexpr (XML) {                                                                   \
+      _Pragma("unroll") for (int rt = 0; rt < RW; ++rt)                                    \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e)                                      \
+          xb[rt][e] = __uint_as_float(__float_as_uint(f4c(f[rt], e)) & msk[e]);            \
+    } else {                                                                               \
+      const double2 s01 = *(const double2*)(sS + k), s23 = *(const double2*)(sS + k + 2);  \
+      const double2 m01 = *(const double2*)(sM + k), m23 = *(const double2*)(sM + k + 2);  \
+      const double sc[4] = {s01.x, s01.y, s23.x, s23.y}, mn[4] = {m01.x, m01.y, m23.x, m23.y}; \
+      _Pragma("unroll") for (int rt = 0; rt < RW; ++rt) {                                  \
+        const double gv[4] = {g[rt][0].x, g[rt][0].y, g[rt][1].x, g[rt][1].y};             \
+        _Pragma("unroll") for (int e = 0; e < 4; ++e)                                      \
+          xb[rt][e] = __uint_as_float(__float_as_uint((float)(gv[e] * sc[e] + mn[e])) & msk[e]); \
+      }                                                                                    \
     }                                                                                      \
     _Pragma("unroll") for (int s = 0; s < 4; ++s)                                          \
       _Pragma("unroll") for (int nb = 0; nb < 4; ++nb)                                     \
@@ -1765,28 +1782,28 @@ __global__ __launch_bounds__(256, RW == 1 ? MV_MLPR_OCC : 2) void k_mlpr(int slo
     // scheduler sinks every load next to its first use (vmcnt(0) before each MFMA group)
     const int nkg0e = (nkg0 + 3) & ~3;
     MR_LOADW(0, wA)
-    MR_LOADG(0, g0)
-    MR_LOADG(1, g1)
-    MR_LOADG(2, g2)
+    MR_LOADG(0, g0, f0)
+    MR_LOADG(1, g1, f1)
+    MR_LOADG(2, g2, f2)
     if (ph) phq[1] = clock64();
 #pragma unroll 1
     for (int kg = 0; kg < nkg0e; kg += 4) {
       MR_LOADW(kg + 1, wB)
-      MR_LOADG(kg + 3, g3)
+      MR_LOADG(kg + 3, g3, f3)
       asm volatile("" ::: "memory");
-      MR_STEP(kg, wA, g0)
+      MR_STEP(kg, wA, g0, f0)
       MR_LOADW(kg + 2, wA)
-      MR_LOADG(kg + 4, g0)
+      MR_LOADG(kg + 4, g0, f0)
       asm volatile("" ::: "memory");
-      MR_STEP(kg + 1, wB, g1)
+      MR_STEP(kg + 1, wB, g1, f1)
       MR_LOADW(kg + 3, wB)
-      MR_LOADG(kg + 5, g1)
+      MR_LOADG(kg + 5, g1, f1)
       asm volatile("" ::: "memory");
-      MR_STEP(kg + 2, wA, g2)
+      MR_STEP(kg + 2, wA, g2, f2)
       MR_LOADW(kg + 4, wA)
-      MR_LOADG(kg + 6, g2)
+      MR_LOADG(kg + 6, g2, f2)
       asm volatile("" ::: "memory");
-      MR_STEP(kg + 3, wB, g3)
+      MR_STEP(kg + 3, wB, g3, f3)
       if (ph && kg == 0) phq[2] = clock64();
     }
     if (ph) phq[3] = clock64();
@@ -2874,14 +2891,14 @@ static hipError_t mlp2_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
                         : mlp2_go3<CJ, BF, false, false>(a, slot, hist_row0, stream);
 }
 
-template <int RW, int NO>
+template <int RW, int NO, bool XML = false>
 static hipError_t mlpr_go(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   static size_t occ_lds = 0;
   static int occ = 1;
   const size_t lds = mlpr_lds(a.p, RW).total;
   if (lds != occ_lds) {  // resident workgroups per CU at this LDS size
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlpr<RW, NO>, 256, lds) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_mlpr<RW, NO, XML>, 256, lds) != hipSuccess ||
         n < 1)
       n = 1;
     (void)hipGetLastError();
@@ -2891,7 +2908,7 @@ static hipError_t mlpr_go(const RowsArgs& a, int slot, int hist_row0, hipStream_
   const int ntiles = (a.total + 16 * RW - 1) / (16 * RW);
   const int need = (ntiles + 3) / 4;
   const int grid = need < occ * cu_count() ? need : occ * cu_count();
-  MV_LAUNCH((k_mlpr<RW, NO>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
+  MV_LAUNCH((k_mlpr<RW, NO, XML>), dim3(grid), dim3(256), lds, stream, slot, hist_row0);
   return hipGetLastError();
 }
 
@@ -2945,7 +2962,7 @@ static bool use_mlpw32(const DProblem& p) {
 // (3, k_mlp2x, was retired), 6 k_mlpr (gene-reading, hidden widths <= 64)
 int mlp_kernel_kind(const DProblem& p) {
   if (p.n_layers == 0) return -1;
-  if (use_mlpr(p)) return 6;
+  if (use_mlpr(p)) return p.xml_direct ? 6 : 7;
   if (p.mlp2 && !std::getenv("MV_MLP_V1") && !(p.mlp_bf16 && std::getenv("MV_MLPW")))
     return p.xml_direct ? 1 : 2;
   if (p.mlp_bf16 && mlpw_lds(p).total <= 160 * 1024 && !std::getenv("MV_MLPW_OFF")) return 4;
@@ -2955,6 +2972,9 @@ int mlp_kernel_kind(const DProblem& p) {
 
 hipError_t launch_mlp(const RowsArgs& a, int slot, int hist_row0, hipStream_t stream) {
   if (a.total <= 0 || a.p.n_layers == 0) return hipSuccess;  // model-less: f1 from the host
+  if (use_mlpr(a.p) && !a.p.xml_direct)  // the fp32 ML rows (LCLD)
+    return a.p.dims[a.p.n_layers] <= 2 ? mlpr_go<1, 2, true>(a, slot, hist_row0, stream)
+                                       : mlpr_go<1, 8, true>(a, slot, hist_row0, stream);
   if (use_mlpr(a.p)) {
     if (a.p.dims[a.p.n_layers] <= 2)
       return mlpr_rw() == 1 ? mlpr_go<1, 2>(a, slot, hist_row0, stream)

@@ -436,7 +436,7 @@ class Engine:
                 "gen_ms": ph[0], "cons_ms": ph[1], "generations": n.value,
                 "row_kernel": ("k_gen+k_cons", "k_narrow", "k_genc")[rk.value],
                 "mlp_kernel": {-1: None, 0: "k_mlp", 1: "k_mlp2(genes)", 2: "k_mlp2",
-                               4: "k_mlpw", 5: "k_mlpw32", 6: "k_mlpr(genes)"}[mk.value]}
+                               4: "k_mlpw", 5: "k_mlpw32", 6: "k_mlpr(genes)", 7: "k_mlpr"}[mk.value]}
 
 
 def survive(F, ref_points, n_survive, mu, seed, gen, ideal, worst, extreme, has_extreme,
